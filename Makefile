@@ -1,0 +1,35 @@
+# Builds the product library, the synthetic packet generator and (via
+# oracle/Makefile) the test oracle.  Everything is built in-tree so the .so
+# files travel to the GPU box with the repo snapshot.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CC       ?= gcc
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+CFLAGS   ?= -O2 -std=gnu11 -fPIC -Wall -Wextra -Wno-unused-parameter
+
+PRODUCT := onload_amd/liboo_gpu_rx.so
+PKTGEN  := onload_amd/liboo_pktgen.so
+SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_gpu_rx.cpp
+HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
+
+all: $(PRODUCT) $(PKTGEN) oracle
+
+$(PRODUCT): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+
+$(PKTGEN): onload_amd/csrc/oo_pktgen.c onload_amd/csrc/oo_pktgen.h include/oo_gpu_rx.h
+	$(CC) $(CFLAGS) -shared -o $@ onload_amd/csrc/oo_pktgen.c
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: $(SRCS) $(HDRS)
+	mkdir -p build
+	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o build/oo_rx_kernel.s onload_amd/csrc/oo_rx_kernel.hip \
+	  -Rpass-analysis=kernel-resource-usage 2> build/resource-usage.txt
+
+clean:
+	rm -f $(PRODUCT) $(PKTGEN)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle asm clean

@@ -1,0 +1,241 @@
+/* SPDX-License-Identifier: BSD-2-Clause */
+/*
+ * oo_gpu_rx.h -- C ABI of the MI355X (gfx950) receive-path transform library.
+ *
+ * The library runs Onload's per-packet software receive transform on a batch
+ * of frames held in GPU memory (HBM):
+ *
+ *   software checksum verify  handle_rx_csum_bad   src/lib/transport/ip/netif_event.c:1014-1128
+ *     IPv4 header csum         ci_ip_csum_correct   netif_event.c:80-94
+ *     TCP csum                 ci_tcp_csum_correct  netif_event.c:97-113
+ *     UDP csum                 ci_udp_csum_correct  src/lib/transport/ip/udp_rx.c:101-121
+ *   header parse               ci_parse_rx_vlan     netif_event.c:116-132
+ *                              handle_rx_pkt        netif_event.c:250-451
+ *                              ci_ip_options_parse  netif_event.c:135-185
+ *   4-tuple socket demux       ci_udp_handle_rx     udp_rx.c:236-307 (2 stages)
+ *                              ci_tcp_handle_rx     src/lib/transport/ip/tcp_rx.c:4681-4836 (3 stages)
+ *                              ci_netif_filter_for_each_match      netif_table.c:234-319
+ *                              ci_netif_filter_for_each_match_ip6  netif_table_ip6.c:110-189
+ *
+ * and returns one fixed 32-byte record per frame (the batched equivalent of the
+ * pre-resolved "future" the RX poll loop already understands,
+ * src/lib/transport/ip/udp_internal.h:27-134, tcp_rx.h:136-214).
+ *
+ * Conventions (same as the reference):
+ *  - addresses and ports are network-order values held in host integers
+ *    ("BE values in host integers"), exactly what a little-endian load of the
+ *    wire bytes yields;
+ *  - 0 or a positive count on success, -errno on failure (ef_vi style);
+ *    per-packet outcomes are reason codes, never errors;
+ *  - every pointer is plain memory owned by the caller unless stated; device
+ *    pointers are HIP device addresses; `stream` is a hipStream_t passed as
+ *    void* (NULL = the null stream).
+ *
+ * Threading: a context belongs to one Onload stack and is used by the holder
+ * of that stack's lock (netif_event.c:1919).  Table updates and batches are
+ * serialised at that lock, like oof's deferred filter ops
+ * (src/lib/efthrm/oof_interface.c:184-217).
+ */
+#ifndef OO_GPU_RX_H
+#define OO_GPU_RX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OO_GPU_RX_ABI_VERSION 1
+
+/* intf_i -> hwport map size (CI_CFG_MAX_INTERFACES = 30,
+ * src/include/ci/internal/transport_config_opt.h:29). */
+#define OO_GPU_RX_MAX_INTF 32
+
+/* ---------------------------------------------------------------------
+ * Per-packet outcome (reason) codes, in the reference's check order.
+ * reason < OO_RX_R_DROP_BASE  => handle_rx_csum_bad() returned 1 (handled)
+ * reason >= OO_RX_R_DROP_BASE => it returned 0: the caller releases the pkt
+ * --------------------------------------------------------------------- */
+enum {
+  OO_RX_R_DELIVER        = 0,  /* socket matched: sock/stage/nmatch valid      */
+  OO_RX_R_NO_MATCH       = 1,  /* udp_rx.c:315-347 / tcp_rx.c:4838-4853       */
+  OO_RX_R_IP4_FRAG       = 2,  /* MF/offset set: netif_event.c:293-295, :339   */
+  OO_RX_R_IP4_OPTS_BAD   = 3,  /* ci_ip_options_parse error: :302-303          */
+  OO_RX_R_TCP_SCATTERED  = 4,  /* frag_off not in {0,DF}: tcp_rx.c:4696-4699   */
+  OO_RX_R_DROP_BASE      = 16,
+  OO_RX_R_SHORT_L2       = 16, /* netif_event.c:1030                            */
+  OO_RX_R_NOT_IP         = 17, /* :1078                                         */
+  OO_RX_R_IP4_LEN        = 18, /* :1047                                         */
+  OO_RX_R_IP4_CSUM       = 19, /* :1054                                         */
+  OO_RX_R_IP6_LEN        = 20, /* :1067                                         */
+  OO_RX_R_PROTO_OTHER    = 21, /* :1121                                         */
+  OO_RX_R_TCP_SHORT      = 22, /* :1087                                         */
+  OO_RX_R_TCP_CSUM       = 23, /* :1091 (incl. doff<5, hlen>ip_paylen)          */
+  OO_RX_R_UDP_SHORT      = 24, /* :1106                                         */
+  OO_RX_R_UDP_CSUM       = 25, /* :1110 (incl. udp_len<8 or >paylen; v6 csum 0) */
+  OO_RX_R_COUNT          = 32
+};
+
+/* Record flags. */
+#define OO_RX_F_IP6     0x01u  /* CI_PKT_FLAG_IS_IP6 (ip_shared_types.h:387)     */
+#define OO_RX_F_VLAN    0x02u  /* 802.1Q tag parsed (netif_event.c:126-130)       */
+#define OO_RX_F_CSUM_OK 0x04u  /* L3+L4 software checksum verified                */
+#define OO_RX_F_MCAST   0x08u  /* daddr multicast/broadcast: host must keep
+                                  delivering to every match (udp_rx.c:148-203)     */
+#define OO_RX_F_MULTI   0x10u  /* nmatch > 1 in the deciding stage               */
+
+/* One frame in the batch.  16 bytes. */
+typedef struct oo_gpu_pkt_desc {
+  uint64_t frame_off;   /* byte offset of the frame's first L2 byte in the
+                           frame buffer (AF_XDP: addr - headroom,
+                           efxdp_vi.c:326-352, netif_event.c:1724-1727)      */
+  uint16_t len;         /* frame length in bytes (no FCS; ef_event.rx.len)  */
+  int16_t  intf_i;      /* Onload interface index (pkt->intf_i)              */
+  uint32_t rsvd;        /* must be 0                                          */
+} oo_gpu_pkt_desc;
+
+/* Per-frame result.  32 bytes, written for every descriptor.
+ *
+ * Fields are defined in stages; anything a stage does not reach is 0 (sock
+ * is -1 unless reason == OO_RX_R_DELIVER):
+ *  - always:                      reason, flags&VLAN, vlan
+ *  - ether_type IPv4/IPv6 and
+ *    frame >= pre_l3 + 20:        flags&IP6, proto, ip_paylen (low 16 bits of
+ *                                 the int the reference computes)
+ *  - handled (reason < 16):       flags&CSUM_OK, l4_off, ports, saddr, daddr
+ *  - lookups ran (DELIVER or
+ *    NO_MATCH):                   hash3 (stage-1 __onload_hash3, rxp.hash),
+ *                                 flags&MCAST
+ *  - DELIVER:                     sock, stage, nmatch, flags&MULTI
+ * For IPv6, saddr/daddr hold onload_addr_xor() of the address (the value the
+ * hash consumes, src/include/onload/hash.h:31-42); the full addresses are in
+ * the frame at l4_off - 32 and l4_off - 16.
+ */
+typedef struct oo_gpu_rx_result {
+  uint8_t  reason;      /* OO_RX_R_*                                         */
+  uint8_t  flags;       /* OO_RX_F_*                                         */
+  uint8_t  stage;       /* 1..3 = deciding lookup stage, 0 = none            */
+  uint8_t  proto;       /* IP protocol / IPv6 next header                    */
+  uint16_t vlan;        /* pkt->vlan (12-bit VID)                            */
+  uint16_t l4_off;      /* L4 header offset from the frame start             */
+  uint16_t ip_paylen;   /* IPv4 tot_len-4*IHL / IPv6 payload_len             */
+  uint16_t sport_be;    /* L4 source port, network order in host integer     */
+  uint16_t dport_be;    /* L4 dest port                                      */
+  uint16_t nmatch;      /* matching filter entries in the deciding stage     */
+  uint32_t saddr_be;    /* IPv4 saddr / IPv6 addr xor-fold                   */
+  uint32_t daddr_be;    /* IPv4 daddr / IPv6 addr xor-fold                   */
+  int32_t  sock;        /* matched socket id (OO_SP) or -1                   */
+  uint32_t hash3;       /* stage-1 __onload_hash3 (tcp rxp.hash)             */
+} oo_gpu_rx_result;
+
+/* Per-reason packet counts for one batch; the host maps them onto Onload's
+ * stats (rx_discard_csum_bad stats_def.h:521, rx_discard_ip_options_bad :537,
+ * udp_rx_no_match_drops :631, rx_sw_csum_pass :881, ...). */
+typedef struct oo_gpu_rx_counters {
+  uint32_t by_reason[OO_RX_R_COUNT];
+} oo_gpu_rx_counters;
+
+/* Socket-side fields the demux reads (netif_table.c:192-231,
+ * netif_table_ip6.c:146-170; accessors src/include/ci/internal/ip.h:1315-1340).
+ * Values are exactly what the reference accessors return for the socket. */
+#define OO_GPU_RX_SOCK_CONNECTED 0x1u  /* CI_SOCK_FLAG_CONNECTED             */
+#define OO_GPU_RX_SOCK_BIND2DEV  0x2u  /* rx_bind2dev_ifindex != CI_IFID_BAD */
+typedef struct oo_gpu_rx_sock {
+  uint32_t raddr_be32;        /* sock_raddr_be32(s)                          */
+  uint16_t rport_be16;        /* sock_rport_be16(s)                          */
+  uint16_t lport_be16;        /* sock_lport_be16(s)                          */
+  uint8_t  protocol;          /* sock_protocol(s)                            */
+  uint8_t  rsvd0;
+  uint16_t flags;             /* OO_GPU_RX_SOCK_*                            */
+  int16_t  bind2dev_vlan;     /* s->rx_bind2dev_vlan                         */
+  uint16_t rsvd1;
+  uint64_t bind2dev_hwports;  /* s->rx_bind2dev_hwports                      */
+  uint8_t  raddr6[16];        /* sock_ip6_raddr(s)                           */
+  uint8_t  rsvd2[8];
+} oo_gpu_rx_sock;             /* 48 bytes                                     */
+
+typedef struct oo_gpu_rx_cfg {
+  int32_t  device;            /* HIP device ordinal; < 0 = host-only context
+                                 (table mirror without a GPU; batch calls
+                                 return -ENODEV)                               */
+  uint32_t max_socks;         /* socket ids are 0..max_socks-1 (EP buffers)  */
+  uint8_t  ip4_table_log2;    /* >= 16 (netif_table.c:280 LPRP), <= 24;
+                                 default 16 (ip.h:1790-1804)                  */
+  uint8_t  ip6_table_log2;    /* 1..24; default 14 (netif_init.c:107-108)    */
+  uint8_t  n_intf;            /* entries used in intf_hwport                 */
+  uint8_t  rsvd;
+  uint8_t  intf_hwport[OO_GPU_RX_MAX_INTF]; /* ni->state->intf_i_to_hwport   */
+  uint64_t host_stage_bytes;  /* frame staging for oo_gpu_rx_batch (0=none)  */
+  uint32_t host_stage_pkts;   /* descriptor/result staging for oo_gpu_rx_batch */
+  uint32_t rsvd2;
+} oo_gpu_rx_cfg;
+
+typedef struct oo_gpu_rx_ctx oo_gpu_rx_ctx;
+
+/* Library / context lifetime. */
+int  oo_gpu_rx_abi_version(void);
+int  oo_gpu_rx_open(oo_gpu_rx_ctx** ctx_out, const oo_gpu_rx_cfg* cfg);
+void oo_gpu_rx_close(oo_gpu_rx_ctx* ctx);
+
+/* Filter-table mirror.  Replaces ci_netif_filter_insert / _remove
+ * (netif_table.c:436-503 -> ci_ip4_netif_filter_insert :323-406,
+ * ci_ip4_netif_filter_remove :447-495; IPv6 netif_table_ip6.c:192-345) for one
+ * address family (af = 4 or 6).  Slot placement, route counts and tombstones
+ * are identical to the reference.  laddr/raddr point at 4 (af 4) or 16 (af 6)
+ * network-order bytes; raddr NULL means the wildcard.
+ * insert: 0, -ENOBUFS (table full, :375), -EINVAL.  remove: 0 (also when the
+ * filter is absent, :476-481), -EINVAL.  Changes reach the device before the
+ * next batch on the context's stream. */
+int oo_gpu_rx_table_insert(oo_gpu_rx_ctx* ctx, int af,
+                           const void* laddr, uint16_t lport_be16,
+                           const void* raddr, uint16_t rport_be16,
+                           uint8_t protocol, int32_t sock_id);
+int oo_gpu_rx_table_remove(oo_gpu_rx_ctx* ctx, int af,
+                           const void* laddr, uint16_t lport_be16,
+                           const void* raddr, uint16_t rport_be16,
+                           uint8_t protocol, int32_t sock_id);
+/* Exact-tuple slot lookup, ci_ip4_netif_filter_lookup (netif_table.c:86-143) /
+ * ci_ip6_netif_filter_lookup (netif_table_ip6.c:13-66): slot index >= 0,
+ * -ENOENT or -ELOOP. */
+int oo_gpu_rx_table_lookup(oo_gpu_rx_ctx* ctx, int af,
+                           const void* laddr, uint16_t lport_be16,
+                           const void* raddr, uint16_t rport_be16,
+                           uint8_t protocol);
+/* Raw view of one table slot for diagnostics/tests: id_state (v4: id|state<<30,
+ * v6: id with -1 tombstone / -2 empty), route_count, lport (v4 ext). */
+int oo_gpu_rx_table_slot(oo_gpu_rx_ctx* ctx, int af, uint32_t slot,
+                         uint32_t* id_state, int32_t* route_count,
+                         uint16_t* lport_be16);
+int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* ctx, int32_t sock_id,
+                       const oo_gpu_rx_sock* sock);
+/* Push pending table/socket changes to the device on `stream` now. */
+int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* ctx, void* stream);
+
+/* Device-resident batch: frames, descriptors and results all in HBM.
+ * Enqueues the transform of n frames on `stream` and returns immediately.
+ * d_counters (device, may be NULL) is incremented per reason.
+ * Returns 0 or -EINVAL. */
+int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* ctx, const void* d_frames,
+                          uint64_t frames_bytes,
+                          const oo_gpu_pkt_desc* d_desc, uint32_t n,
+                          oo_gpu_rx_result* d_out,
+                          oo_gpu_rx_counters* d_counters, void* stream);
+
+/* Host-memory batch (the NIC ring -> socket path): copies frames and
+ * descriptors host->device, runs the transform, copies results (and the
+ * per-reason deltas, if `delta` is not NULL) back, and waits.  Frame bytes
+ * and n must fit the staging sizes given at open.  Returns n or -errno. */
+int oo_gpu_rx_batch(oo_gpu_rx_ctx* ctx, const void* frames,
+                    uint64_t frames_bytes, const oo_gpu_pkt_desc* desc,
+                    uint32_t n, oo_gpu_rx_result* out,
+                    oo_gpu_rx_counters* delta);
+
+/* Reason code -> short name ("DELIVER", "UDP_CSUM", ...). */
+const char* oo_gpu_rx_reason_str(int reason);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OO_GPU_RX_H */

@@ -1,0 +1,147 @@
+# SPDX-License-Identifier: BSD-2-Clause
+"""ctypes/numpy mirror of the C ABI in include/oo_gpu_rx.h.
+
+Loads the in-tree gfx950 library ``onload_amd/liboo_gpu_rx.so`` and fails
+loudly when it is missing: there is no CPU fallback for the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboo_gpu_rx.so")
+PKTGEN_PATH = os.path.join(_HERE, "liboo_pktgen.so")
+
+ABI_VERSION = 1
+MAX_INTF = 32
+
+# Reason codes (oo_gpu_rx.h), in the reference's check order.
+R_DELIVER, R_NO_MATCH, R_IP4_FRAG, R_IP4_OPTS_BAD, R_TCP_SCATTERED = 0, 1, 2, 3, 4
+R_DROP_BASE = 16
+R_SHORT_L2, R_NOT_IP, R_IP4_LEN, R_IP4_CSUM, R_IP6_LEN = 16, 17, 18, 19, 20
+R_PROTO_OTHER, R_TCP_SHORT, R_TCP_CSUM, R_UDP_SHORT, R_UDP_CSUM = 21, 22, 23, 24, 25
+R_COUNT = 32
+REASON_NAMES = {
+    0: "DELIVER", 1: "NO_MATCH", 2: "IP4_FRAG", 3: "IP4_OPTS_BAD", 4: "TCP_SCATTERED",
+    16: "SHORT_L2", 17: "NOT_IP", 18: "IP4_LEN", 19: "IP4_CSUM", 20: "IP6_LEN",
+    21: "PROTO_OTHER", 22: "TCP_SHORT", 23: "TCP_CSUM", 24: "UDP_SHORT", 25: "UDP_CSUM",
+}
+
+F_IP6, F_VLAN, F_CSUM_OK, F_MCAST, F_MULTI = 0x01, 0x02, 0x04, 0x08, 0x10
+SOCK_CONNECTED, SOCK_BIND2DEV = 0x1, 0x2
+
+DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("len", "<u2"), ("intf_i", "<i2"),
+                       ("rsvd", "<u4")])
+RESULT_DTYPE = np.dtype([
+    ("reason", "u1"), ("flags", "u1"), ("stage", "u1"), ("proto", "u1"),
+    ("vlan", "<u2"), ("l4_off", "<u2"), ("ip_paylen", "<u2"), ("sport_be", "<u2"),
+    ("dport_be", "<u2"), ("nmatch", "<u2"), ("saddr_be", "<u4"), ("daddr_be", "<u4"),
+    ("sock", "<i4"), ("hash3", "<u4")])
+assert DESC_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 32
+
+
+class Sock(ctypes.Structure):
+    """oo_gpu_rx_sock: the socket-side fields the demux reads."""
+    _fields_ = [("raddr_be32", ctypes.c_uint32), ("rport_be16", ctypes.c_uint16),
+                ("lport_be16", ctypes.c_uint16), ("protocol", ctypes.c_uint8),
+                ("rsvd0", ctypes.c_uint8), ("flags", ctypes.c_uint16),
+                ("bind2dev_vlan", ctypes.c_int16), ("rsvd1", ctypes.c_uint16),
+                ("bind2dev_hwports", ctypes.c_uint64), ("raddr6", ctypes.c_uint8 * 16),
+                ("rsvd2", ctypes.c_uint8 * 8)]
+
+
+class Cfg(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_socks", ctypes.c_uint32),
+                ("ip4_table_log2", ctypes.c_uint8), ("ip6_table_log2", ctypes.c_uint8),
+                ("n_intf", ctypes.c_uint8), ("rsvd", ctypes.c_uint8),
+                ("intf_hwport", ctypes.c_uint8 * MAX_INTF),
+                ("host_stage_bytes", ctypes.c_uint64), ("host_stage_pkts", ctypes.c_uint32),
+                ("rsvd2", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(Sock) == 48
+
+
+class PgFilter(ctypes.Structure):
+    """oo_pg_filter (onload_amd/csrc/oo_pktgen.h)."""
+    _fields_ = [("sock", ctypes.c_int32), ("af", ctypes.c_uint8), ("proto", ctypes.c_uint8),
+                ("lport_be", ctypes.c_uint16), ("rport_be", ctypes.c_uint16),
+                ("raddr_any", ctypes.c_uint8), ("rsvd", ctypes.c_uint8),
+                ("laddr", ctypes.c_uint8 * 16), ("raddr", ctypes.c_uint8 * 16)]
+
+
+# Every symbol include/oo_gpu_rx.h declares, with its ctypes signature.
+_P, _U8, _U16, _U32, _U64, _I32 = (ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16,
+                                   ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32)
+ABI_SYMBOLS = {
+    "oo_gpu_rx_abi_version": (ctypes.c_int, []),
+    "oo_gpu_rx_open": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(Cfg)]),
+    "oo_gpu_rx_close": (None, [_P]),
+    "oo_gpu_rx_table_insert": (ctypes.c_int, [_P, ctypes.c_int, _P, _U16, _P, _U16, _U8, _I32]),
+    "oo_gpu_rx_table_remove": (ctypes.c_int, [_P, ctypes.c_int, _P, _U16, _P, _U16, _U8, _I32]),
+    "oo_gpu_rx_table_lookup": (ctypes.c_int, [_P, ctypes.c_int, _P, _U16, _P, _U16, _U8]),
+    "oo_gpu_rx_table_slot": (ctypes.c_int, [_P, ctypes.c_int, _U32, ctypes.POINTER(_U32),
+                                            ctypes.POINTER(_I32), ctypes.POINTER(_U16)]),
+    "oo_gpu_rx_sock_set": (ctypes.c_int, [_P, _I32, ctypes.POINTER(Sock)]),
+    "oo_gpu_rx_sync_tables": (ctypes.c_int, [_P, _P]),
+    "oo_gpu_rx_process_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _P]),
+    "oo_gpu_rx_batch": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P]),
+    "oo_gpu_rx_reason_str": (ctypes.c_char_p, [ctypes.c_int]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the gfx950 library.  Raises if it was not built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"onload_amd: {path} is missing; build it with `make` (hipcc --offload-arch=gfx950). "
+            "There is no CPU fallback for the receive transform.")
+    try:  # share torch's HIP runtime when torch is present (same soname)
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is part of the image
+        pass
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in ABI_SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.oo_gpu_rx_abi_version() != ABI_VERSION:
+        raise RuntimeError("onload_amd: ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+_pg = None
+
+
+def load_pktgen(path: str = PKTGEN_PATH) -> ctypes.CDLL:
+    global _pg
+    if _pg is not None:
+        return _pg
+    if not os.path.exists(path):
+        raise RuntimeError(f"onload_amd: {path} is missing; run `make`")
+    lib = ctypes.CDLL(path)
+    lib.oo_pg_default_seed.restype = ctypes.c_uint64
+    lib.oo_pg_default_seed.argtypes = [ctypes.c_int]
+    lib.oo_pg_world.restype = ctypes.c_int
+    lib.oo_pg_world.argtypes = [ctypes.c_int, ctypes.POINTER(PgFilter), ctypes.c_int,
+                                ctypes.POINTER(Sock), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    lib.oo_pg_len.restype = ctypes.c_uint32
+    lib.oo_pg_len.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+    lib.oo_pg_bytes.restype = ctypes.c_uint64
+    lib.oo_pg_bytes.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                ctypes.c_uint32]
+    lib.oo_pg_gen.restype = ctypes.c_uint64
+    lib.oo_pg_gen.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                              ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                              ctypes.c_int]
+    _pg = lib
+    return lib

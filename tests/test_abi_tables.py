@@ -1,0 +1,128 @@
+# SPDX-License-Identifier: BSD-2-Clause
+"""C-ABI library: loads, exports every symbol include/oo_gpu_rx.h declares,
+struct layouts match the header, and the host-side filter-table mirror
+(host-only context, no GPU needed) places entries exactly like the oracle's
+restatement of netif_table.c / netif_table_ip6.c."""
+import ctypes
+import errno
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from onload_amd import _abi
+from onload_amd.rx import GpuRxStack
+from oracle_lib import OracleStack
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "oo_gpu_rx.h")
+
+
+def test_header_symbols_exported():
+    text = open(HDR).read()
+    declared = set(re.findall(r"\b(oo_gpu_rx_\w+)\s*\(", text))
+    assert declared == set(_abi.ABI_SYMBOLS), declared ^ set(_abi.ABI_SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (oo_gpu_rx_\w+)", out))
+    assert declared <= exported, declared - exported
+    lib = _abi.load_library()
+    assert lib.oo_gpu_rx_abi_version() == _abi.ABI_VERSION
+    assert lib.oo_gpu_rx_reason_str(25) == b"UDP_CSUM"
+
+
+def test_layouts_match_header(tmp_path):
+    src = tmp_path / "l.c"
+    src.write_text('#include "oo_gpu_rx.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                   "int main(void){printf(\"%zu %zu %zu %zu %zu %zu\\n\","
+                   "sizeof(oo_gpu_pkt_desc),sizeof(oo_gpu_rx_result),sizeof(oo_gpu_rx_sock),"
+                   "sizeof(oo_gpu_rx_cfg),offsetof(oo_gpu_rx_result,sock),"
+                   "offsetof(oo_gpu_rx_cfg,host_stage_bytes));return 0;}\n")
+    exe = tmp_path / "l"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got == [_abi.DESC_DTYPE.itemsize, _abi.RESULT_DTYPE.itemsize, ctypes.sizeof(_abi.Sock),
+                   ctypes.sizeof(_abi.Cfg), _abi.RESULT_DTYPE.fields["sock"][1],
+                   _abi.Cfg.host_stage_bytes.offset]
+
+
+def test_open_rejects_bad_config():
+    lib = _abi.load_library()
+    cfg = _abi.Cfg()
+    cfg.device = -1
+    cfg.max_socks = 16
+    cfg.ip4_table_log2 = 15  # < 16 breaks the LPRP fast path (netif_table.c:280)
+    cfg.ip6_table_log2 = 4
+    ctx = ctypes.c_void_p()
+    assert lib.oo_gpu_rx_open(ctypes.byref(ctx), ctypes.byref(cfg)) == -errno.EINVAL
+
+
+def test_host_only_context_has_no_device_path():
+    st = GpuRxStack(device=-1, max_socks=16, ip6_log2=4)
+    with pytest.raises(OSError) as e:
+        st.handle_rx_batch_dev(1, 1, 1, 1, 1)
+    assert e.value.errno == errno.ENODEV
+    assert st.filter_insert(99, 4, "1.2.3.4", 1, None, 0, 17) == -errno.EINVAL  # bad sock id
+
+
+def _random_ops(rng, n, af, n_socks, small_ports):
+    ops = []
+    live = []
+    for k in range(n):
+        if live and rng.random() < 0.35:
+            ops.append(("rm",) + live.pop(int(rng.integers(len(live)))))
+            continue
+        sid = int(rng.integers(n_socks))
+        if af == 4:
+            la = bytes([10, 0, 0, int(rng.integers(1, 4))])
+            ra = None if rng.random() < 0.5 else bytes([10, 1, int(rng.integers(256)),
+                                                         int(rng.integers(256))])
+        else:
+            la = bytes([0xfd] + [0] * 14 + [int(rng.integers(1, 4))])
+            ra = None if rng.random() < 0.5 else bytes([0xfd, 9] + list(rng.integers(0, 256, 14)))
+        lp = int(rng.integers(small_ports))
+        rp = 0 if ra is None else int(rng.integers(1, 65536))
+        proto = 6 if rng.random() < 0.5 else 17
+        t = (sid, af, la, lp, ra, rp, proto)
+        ops.append(("ins",) + t)
+        live.append(t)
+    return ops
+
+
+@pytest.mark.parametrize("af,log2,nops", [(4, 16, 6000), (6, 6, 3000), (6, 3, 400)])
+def test_table_mirror_matches_oracle(af, log2, nops):
+    """Insert/remove scripts with tombstones, route counts, re-insert over
+    tombstones and a full table (-ENOBUFS)."""
+    rng = np.random.default_rng(af * 100 + log2)
+    n_socks = 512
+    g = GpuRxStack(device=-1, max_socks=n_socks, ip4_log2=16 if af == 6 else log2,
+                   ip6_log2=log2 if af == 6 else 4)
+    o = OracleStack(max_socks=n_socks, ip4_log2=16 if af == 6 else log2,
+                    ip6_log2=log2 if af == 6 else 4)
+    socks = [_abi.Sock() for _ in range(n_socks)]
+    for i, s in enumerate(socks):
+        s.protocol = 6 if i % 2 else 17
+        s.rport_be16 = i
+        assert g.sock_set(i, s) == 0 and o.sock_set(i, s) == 0
+    saw_full = False
+    for op in _random_ops(rng, nops, af, n_socks, 40 if af == 6 else 2000):
+        kind, args = op[0], op[1:]
+        if kind == "ins":
+            a, b = g.filter_insert(*args), o.filter_insert(*args)
+            assert a == b, (op, a, b)
+            saw_full |= a == -errno.ENOBUFS
+        else:
+            assert g.filter_remove(*args) == o.filter_remove(*args) == 0
+    size = 1 << log2
+    for slot in range(size):
+        assert g.table_slot(af, slot) == o.table_slot(af, slot), slot
+    if af == 6 and log2 == 3:
+        assert saw_full
+    # exact lookups agree too
+    for op in _random_ops(rng, 300, af, n_socks, 40 if af == 6 else 2000):
+        args = op[2:]
+        assert g.filter_lookup(*args) == o.filter_lookup(*args)

@@ -1,0 +1,162 @@
+# SPDX-License-Identifier: BSD-2-Clause
+"""Parity of the gfx950 kernels (through the C ABI) with the oracle:
+bit-exact 32-byte records on identical frame buffers, plus counters."""
+import os
+
+import numpy as np
+import pytest
+
+import cases
+from frames import edge_frames, edge_world, install, pack
+from gpu_util import diff_report, run_dev
+from onload_amd import _abi, pktgen
+from onload_amd.rx import GpuRxStack
+from oracle_lib import OracleStack, counters_of
+
+pytestmark = pytest.mark.gpu
+
+NTHREADS = min(16, os.cpu_count() or 1)
+HWPORTS = (0, 1, 3, 2, 5)  # intf 2 -> hwport 3 (edge world's bind2dev socket)
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _pair(world_installer, **kw):
+    g = GpuRxStack(device=0, **kw)
+    o = OracleStack(**kw)
+    world_installer(g)
+    world_installer(o)
+    return g, o
+
+
+def _check(g, o, buf, desc, frames_bytes=None):
+    got, ctr = run_dev(g, buf, desc, frames_bytes)
+    want = o.handle_rx_batch(buf, desc, nthreads=NTHREADS)
+    assert got.tobytes() == want.tobytes(), diff_report(got, want, desc)
+    np.testing.assert_array_equal(ctr, counters_of(want))
+    return got
+
+
+def test_survey_cases_on_gpu(cuda):
+    g, o = _pair(lambda s: install(s, cases.survey_world()))
+    frames = [(f, intf) for (_, f, intf, _) in cases.survey_cases()]
+    buf, desc = pack(frames)
+    got = _check(g, o, buf, desc)
+    for r, (name, _, _, want) in zip(got, cases.survey_cases()):
+        for k, v in want.items():
+            assert r[k] == v, (name, k)
+
+
+def test_lookup_order_on_gpu(cuda):
+    socks, filters = cases.order_world()
+    g, o = _pair(lambda s: install(s, (socks, filters)))
+    buf, desc = pack([(cases.order_frame(), 0)])
+    for stage in (1, 2, 3):
+        r = _check(g, o, buf, desc)[0]
+        assert r["stage"] == stage
+        g.filter_remove(*filters[stage - 1])
+        o.filter_remove(*filters[stage - 1])
+    assert _check(g, o, buf, desc)[0]["reason"] == _abi.R_NO_MATCH
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3, 6, 8, 15])
+def test_edge_corpus(cuda, shift):
+    """Every gate of SURVEY §8(a) on both sides, at every frame alignment
+    (odd offsets exercise the RFC 1071 byte-swap path)."""
+    g, o = _pair(lambda s: install(s, edge_world()), intf_hwport=HWPORTS)
+    buf, desc = pack(edge_frames(), align=64 if shift % 2 == 0 else 16, shift=shift)
+    got = _check(g, o, buf, desc)
+    assert len(set(got["reason"].tolist())) >= 15
+
+
+def test_edge_corpus_shuffled_and_unaligned_tail(cuda):
+    """Random order, random 1-byte offsets, frames abutting the buffer end."""
+    g, o = _pair(lambda s: install(s, edge_world()), intf_hwport=HWPORTS)
+    fr = edge_frames(seed=99)
+    rng = np.random.default_rng(3)
+    chunks, desc, off = [], np.zeros(len(fr), dtype=_abi.DESC_DTYPE), 0
+    for i in rng.permutation(len(fr)):
+        f, intf = fr[i]
+        pad = int(rng.integers(0, 5))
+        chunks.append(bytes(pad) + f)
+        desc[len(chunks) - 1] = (off + pad, len(f), intf, 0)
+        off += pad + len(f)
+    buf = np.frombuffer(b"".join(chunks), dtype=np.uint8).copy()
+    _check(g, o, buf, desc, frames_bytes=len(buf))
+
+
+def test_descriptor_outside_buffer_is_empty_frame(cuda):
+    g, o = _pair(lambda s: install(s, edge_world()))
+    buf, desc = pack(edge_frames()[:10])
+    desc[3]["frame_off"] = len(buf) + 100
+    got, _ = run_dev(g, buf, desc)
+    assert got[3]["reason"] == _abi.R_SHORT_L2
+    mask = np.ones(len(desc), bool)
+    mask[3] = False
+    want = o.handle_rx_batch(buf, desc[mask])
+    assert got[mask].tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("config,n", [(2, 1 << 16), (3, 1 << 18), (4, 1 << 14), (5, 1 << 17)])
+def test_config_samples(cuda, config, n):
+    filters, socks = pktgen.world(config)
+    g, o = _pair(lambda s: s.load_world(filters, socks))
+    first = 12345 * config  # an arbitrary shard
+    buf, desc = pktgen.generate(config, n, first=first)
+    got = _check(g, o, buf, desc)
+    r = got["reason"]
+    assert (r == _abi.R_DELIVER).mean() > 0.8
+    if config in (4, 5):
+        assert set(np.unique(got["stage"][r == 0]).tolist()) == {1, 2, 3}
+
+
+def test_host_path_matches_device_path(cuda):
+    filters, socks = pktgen.world(5)
+    buf, desc = pktgen.generate(5, 4096)
+    g = GpuRxStack(device=0, host_stage_bytes=len(buf), host_stage_pkts=len(desc))
+    g.load_world(filters, socks)
+    a, ca = g.handle_rx_batch(buf, desc)
+    b, cb = run_dev(g, buf, desc)
+    assert a.tobytes() == b.tobytes()
+    np.testing.assert_array_equal(ca, cb)
+
+
+def test_table_updates_reach_device_between_batches(cuda):
+    g, o = _pair(lambda s: install(s, cases.survey_world()))
+    frames = [(f, i) for (_, f, i, _) in cases.survey_cases()]
+    buf, desc = pack(frames)
+    _check(g, o, buf, desc)
+    for s in (g, o):  # connect a UDP socket to the peer: stage 1 now wins
+        s.sock_set(40, cases._sock(17, 6003, cases.PEER, 33000, flags=_abi.SOCK_CONNECTED))
+        assert s.filter_insert(40, 4, cases.LA, 6003, cases.PEER, 33000, 17) == 0
+    got = _check(g, o, buf, desc)
+    assert got[0]["stage"] == 1 and got[0]["sock"] == 40
+    for s in (g, o):
+        s.filter_remove(3, 4, cases.LA, 6003, None, 0, 17)
+    _check(g, o, buf, desc)
+
+
+def test_full_size_config2_bit_exact(cuda):
+    """BASELINE config 2 at full size: 2^20 x 1514 B, every record."""
+    filters, socks = pktgen.world(2)
+    g, o = _pair(lambda s: s.load_world(filters, socks))
+    buf, desc = pktgen.generate(2, 1 << 20)
+    got = _check(g, o, buf, desc)
+    frac = np.bincount(got["reason"], minlength=32) / len(got)
+    assert abs(frac[_abi.R_UDP_CSUM] - 0.01) < 0.002
+    assert abs(frac[_abi.R_NO_MATCH] - 0.005) < 0.002
+    assert frac[_abi.R_DELIVER] > 0.98
+
+
+def test_full_size_config3_properties(cuda):
+    """BASELINE config 3 at 2^22 x 64 B (1/4 of full size) bit-exact."""
+    filters, socks = pktgen.world(3)
+    g, o = _pair(lambda s: s.load_world(filters, socks))
+    buf, desc = pktgen.generate(3, 1 << 22)
+    got = _check(g, o, buf, desc)
+    assert (got["stage"][got["reason"] == 0] == 2).all()
