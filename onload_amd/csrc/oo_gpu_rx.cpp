@@ -28,6 +28,7 @@
 #include "oo_rx_device.h"
 
 extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
+extern "C" int oo_rx_blocks_per_cu(void);
 
 namespace {
 
@@ -344,7 +345,11 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
-    c->grid_cap = prop.multiProcessorCount * 8;
+  {
+    // Persistent grid: exactly the resident blocks (tiles are grid-strided).
+    const int per_cu = oo_rx_blocks_per_cu();
+    c->grid_cap = prop.multiProcessorCount * (per_cu > 0 ? per_cu : 4);
+  }
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_ip4, sizeof(Entry4) * c->ip4.size()) == hipSuccess &&
             hipMalloc(&c->d_ip4_ext, sizeof(Ext4) * c->ip4_ext.size()) == hipSuccess &&

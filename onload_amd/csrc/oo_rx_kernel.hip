@@ -1,6 +1,6 @@
 // SPDX-License-Identifier: BSD-2-Clause
 //
-// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernels for Onload's software
+// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernel for Onload's software
 // receive transform: checksum verify + header parse + 4-tuple socket demux.
 //
 // Reference semantics (file:line in /root/reference):
@@ -17,24 +17,31 @@
 //   ci_netif_filter_for_each_match[_ip6]  netif_table.c:234-319, netif_table_ip6.c:110-189
 //   __onload_hash1/2/3            src/include/onload/hash.h:84-173
 //
-// Execution model (DESIGN.md "Kernel"):
-//  * One persistent-style grid; each wave owns tiles of 64 descriptors.
-//  * Per tile, one coalesced 16-B-per-lane descriptor load; a wave ballot +
-//    mbcnt prefix splits the tile into SMALL frames (whole frame inside one
-//    256-byte window: 4 lanes per packet, 16 packets per wave-pass) and LARGE
-//    frames (one wave per packet, 2 KiB per round, as many rounds as needed).
-//  * Frame bytes are read once from HBM with 16-byte loads into VGPRs; the
-//    first 160 bytes of each packet are also copied to a per-group LDS window,
-//    from which the (group-uniform) header walk reads its fields.
-//  * One's-complement sums use v_dot2_u32_u16 with per-word 0/1 multipliers,
-//    so the region masks cost no byte shuffling; the verdict is the
-//    mod-0xffff residue of the exact word sum (see oracle/rx_oracle.c for why
-//    that equals the reference's folded-complement test).
-//  * The 2 (UDP) or 3 (TCP) filter-table lookup stages run in parallel on
-//    lanes 0..2 of the packet's group; the first stage with a match decides.
-//  * Per-reason counters accumulate in LDS and are flushed once per block.
+// Execution model (DESIGN.md "Kernel"): each wave owns tiles of 64 packets,
+// one packet per lane for everything that is per-packet and latency-bound,
+// and 16-lane rows for the byte stream:
 //
-// No MFMA: this is integer reduction and table probing, HBM-bound.
+//  1. one coalesced 16-B descriptor load per lane;
+//  2. header staging: the first 128 window bytes of the 64 frames are read
+//     with coalesced 16-B loads (8 lanes x 16 B per frame per instruction)
+//     and written transposed into LDS as [chunk][packet] cells, so that
+//  3. every lane parses its own packet's headers from LDS (VLAN, IPv4/IPv6
+//     gates, L4 gates, pseudo-header) and sums the IPv4 header and the part
+//     of the L4 region inside those 128 bytes;
+//  4. packets whose L4 region extends past 128 bytes are streamed by 16-lane
+//     rows (4 packets at a time per wave), 8 x 16-B loads per lane in flight,
+//     one's-complement partial sums by v_dot2_u32_u16 and a DPP row
+//     reduction (no LDS traffic);
+//  5. every lane finishes its packet: verdict, IPv4 frag/options/TCP
+//     scattered tests, the 2 or 3 filter-table lookup stages
+//     (double-hashed probe walks, all 64 lanes' walks in flight together),
+//     and one 32-byte record.
+//  Per-reason counters accumulate in LDS and are flushed once per block.
+//
+// The one's-complement verdict uses the mod-0xffff residue of the exact word
+// sum; oracle/rx_oracle.c explains why it equals the reference's
+// folded-complement test.  No MFMA: integer reduction + table probes,
+// HBM-bound.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -46,11 +53,12 @@ namespace oo_rx {
 typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Streaming 16-byte load (frame bytes are read exactly once).
-__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
+constexpr int WAVES = 4;             // waves per block
+constexpr int HC = 8;                // staged header chunks per packet
+constexpr int HB = HC * 16;          // staged window bytes per packet
+constexpr int ROWB = 64 * 16 + 16;   // one staged chunk of all 64 packets (+pad)
+constexpr int SG = 16;               // lanes per streaming group (one DPP row)
+constexpr int SU = 8;                // 16-B chunks per lane per streaming round
 
 // Filter-table entry states (netif_table.c:34-42).
 constexpr uint32_t ST_MASK = 0xc0000000u;
@@ -59,6 +67,19 @@ constexpr uint32_t ST_PREFERRED = 0x00000000u;
 constexpr uint32_t ST_EMPTY = 0x80000000u;
 constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
 constexpr int ID6_EMPTY = -2;
+constexpr uint32_t PENDING = 0xffu;
+
+struct WaveLds {
+  uint8_t hdr[HC][ROWB];  // staged headers, [chunk][packet] 16-B cells
+  uint4 meta[64];         // streaming job: {abase lo, abase hi, E4, -}
+  uint32_t ssum[64];      // streamed L4 partial sums
+  uint8_t jobs[64];       // streaming job list (lane ids)
+};
+
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 __device__ __forceinline__ bool occupied(uint32_t st) {
   return ((~st) & ST_EMPTY & ST_TOMBSTONE) != 0;
@@ -70,14 +91,10 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) {
-  return __builtin_bswap32(x);
-}
-
 // hash.h:84-93 / 165-173; network-order values in host integers.
 __device__ __forceinline__ uint32_t hash3(uint32_t la, uint32_t lp, uint32_t ra,
                                           uint32_t rp, uint32_t proto) {
-  uint32_t h = bswap32(ra) ^ la ^ ((rp << 16) | lp) ^ proto;
+  uint32_t h = __builtin_bswap32(ra) ^ la ^ ((rp << 16) | lp) ^ proto;
   h ^= h >> 16;
   h ^= h >> 8;
   return h;
@@ -93,52 +110,60 @@ __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   return s;
 }
 
-// Sum of the little-endian u16 words of one 16-byte chunk whose first byte is
-// at window position p, restricted to window byte range [S, E).  Words are
-// paired at even window positions; an odd S or E clips half a word, which is
-// removed by subtracting that byte (it was counted as the word's low byte at
-// S-1, or high byte at E).
+__device__ __forceinline__ uint32_t dot(uint32_t w, uint32_t m, uint32_t acc) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(v2u16, w), __builtin_bit_cast(v2u16, m),
+                                acc, false);
+}
+
+// Sum of all eight LE u16 words of a chunk.
+__device__ __forceinline__ uint32_t chunk_sum_all(const uint4& v, uint32_t acc) {
+  acc = dot(v.x, 0x00010001u, acc);
+  acc = dot(v.y, 0x00010001u, acc);
+  acc = dot(v.z, 0x00010001u, acc);
+  return dot(v.w, 0x00010001u, acc);
+}
+
+// Sum of the LE u16 words of one 16-byte chunk at window position p,
+// restricted to window bytes [S, E).  Words pair at even window positions;
+// an odd S or E clips half a word, removed by subtracting that byte (the low
+// byte of the word at S-1, or the high byte of the word at E-1).
 __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int E) {
   int lo = (S & ~1) - p;
   int hi = ((E + 1) & ~1) - p;
   lo = lo < 0 ? 0 : lo;
   hi = hi > 16 ? 16 : hi;
   uint32_t wm = 0;
-  if (hi > lo)
-    wm = ((1u << (hi >> 1)) - 1u) & ~((1u << (lo >> 1)) - 1u);
-  const v2u16 m0 = __builtin_bit_cast(v2u16, (wm & 1u) | ((wm & 2u) << 15));
-  const v2u16 m1 = __builtin_bit_cast(v2u16, ((wm >> 2) & 1u) | (((wm >> 3) & 1u) << 16));
-  const v2u16 m2 = __builtin_bit_cast(v2u16, ((wm >> 4) & 1u) | (((wm >> 5) & 1u) << 16));
-  const v2u16 m3 = __builtin_bit_cast(v2u16, ((wm >> 6) & 1u) | (((wm >> 7) & 1u) << 16));
+  if (hi > lo) wm = ((1u << (hi >> 1)) - 1u) & ~((1u << (lo >> 1)) - 1u);
   uint32_t s = 0;
-  s = __builtin_amdgcn_udot2(__builtin_bit_cast(v2u16, v.x), m0, s, false);
-  s = __builtin_amdgcn_udot2(__builtin_bit_cast(v2u16, v.y), m1, s, false);
-  s = __builtin_amdgcn_udot2(__builtin_bit_cast(v2u16, v.z), m2, s, false);
-  s = __builtin_amdgcn_udot2(__builtin_bit_cast(v2u16, v.w), m3, s, false);
+  s = dot(v.x, (wm & 1u) | ((wm & 2u) << 15), s);
+  s = dot(v.y, ((wm >> 2) & 1u) | ((wm & 8u) << 13), s);
+  s = dot(v.z, ((wm >> 4) & 1u) | ((wm & 32u) << 11), s);
+  s = dot(v.w, ((wm >> 6) & 1u) | ((wm & 128u) << 9), s);
   if (((S | E) & 1) != 0) {
-    // Rare: odd boundary inside this chunk.
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     if ((S & 1) && S - 1 >= p && S - 1 < p + 16) {
-      int b = S - 1 - p;
+      const int b = S - 1 - p;
       s -= (w[b >> 2] >> ((b & 3) * 8)) & 0xffu;
     }
     if ((E & 1) && E >= p && E < p + 16) {
-      int b = E - p;
+      const int b = E - p;
       s -= ((w[b >> 2] >> ((b & 3) * 8)) & 0xffu) << 8;
     }
   }
   return s;
 }
 
-template <int W>
-__device__ __forceinline__ uint32_t seg_sum(uint32_t v) {
-#pragma unroll
-  for (int o = W / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, W);
+// Inclusive sum over a 16-lane DPP row; lane 15 of the row holds the total.
+__device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);  // row_shr:8
   return v;
 }
 
 // ---------------------------------------------------------------------------
-// Demux: one lookup stage, walked to its end (every match counted).
+// Demux: one lookup stage walked to its end (every match counted).
 
 struct Match {
   int32_t first;
@@ -148,22 +173,24 @@ struct Match {
 __device__ __forceinline__ bool bind2dev_ok(const KParams& P, const oo_gpu_rx_sock& s,
                                             int intf_i, int vlan) {
   if (!(s.flags & OO_GPU_RX_SOCK_BIND2DEV)) return true;
-  uint32_t hw = (intf_i >= 0 && intf_i < OO_GPU_RX_MAX_INTF) ? P.hwport[intf_i] : 0xffu;
+  const uint32_t hw =
+      (intf_i >= 0 && intf_i < OO_GPU_RX_MAX_INTF) ? P.hwport[intf_i] : 0xffu;
   return hw < 64 && (s.bind2dev_hwports & (1ull << hw)) != 0 && s.bind2dev_vlan == vlan;
 }
 
 __device__ __forceinline__ oo_gpu_rx_sock load_sock(const KParams& P, uint32_t id) {
   const uint4* p = reinterpret_cast<const uint4*>(P.socks + id);
-  uint4 a = p[0], b = p[1], c = p[2];
   oo_gpu_rx_sock s;
   uint4* d = reinterpret_cast<uint4*>(&s);
-  d[0] = a; d[1] = b; d[2] = c;
+  d[0] = p[0];
+  d[1] = p[1];
+  d[2] = p[2];
   return s;
 }
 
 // ci_netif_filter_for_each_match (netif_table.c:234-319).
-__device__ Match walk4(const KParams& P, uint32_t la, uint32_t lp, uint32_t ra,
-                       uint32_t rp, uint32_t proto, int intf_i, int vlan) {
+__device__ Match walk4(const KParams& P, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
+                       uint32_t proto, int intf_i, int vlan) {
   Match m = {-1, 0};
   const uint32_t mask = P.ip4_mask;
   uint32_t h1 = hash3(la, lp, ra, rp, proto) & mask;
@@ -195,9 +222,8 @@ __device__ Match walk4(const KParams& P, uint32_t la, uint32_t lp, uint32_t ra,
 }
 
 // ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189).
-__device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp,
-                       const uint32_t ra[4], bool ra_null, uint32_t rp,
-                       uint32_t proto, int intf_i, int vlan) {
+__device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp, const uint32_t ra[4],
+                       bool ra_null, uint32_t rp, uint32_t proto, int intf_i, int vlan) {
   Match m = {-1, 0};
   const uint32_t mask = P.ip6_mask;
   const uint32_t lx = la[0] ^ la[1] ^ la[2] ^ la[3];
@@ -237,307 +263,6 @@ __device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp,
 }
 
 // ---------------------------------------------------------------------------
-// One packet processed by a group of G consecutive lanes (G in {4, 64}).
-// `win` is this group's 16-byte-aligned LDS header window (WIN bytes).
-// All header decisions are group-uniform; lane gl of the group holds frame
-// chunks gl, gl+G, gl+2G, ... (16 bytes each) of every round.
-
-struct PktIn {
-  uint64_t off;   // frame_off
-  uint32_t len;   // frame length (0 for an inactive group)
-  int32_t intf_i;
-  uint32_t idx;   // output record index
-  bool active;
-};
-
-template <int G, int CH>
-__device__ void process_packet(const KParams& P, const PktIn& in, int gl,
-                               uint8_t* __restrict__ win, uint32_t* __restrict__ lds_ctr) {
-  constexpr int RB = G * CH * 16;  // bytes per load round
-  static_assert(RB >= 256, "round 0 must cover the header window");
-
-  const uint32_t len = in.len;
-  const uint8_t* base = P.frames + in.off;
-  const int shift = (int)(reinterpret_cast<uintptr_t>(base) & 15u);
-  const uint4* abase = reinterpret_cast<const uint4*>(base - shift);
-  const int span = shift + (int)len;  // window bytes holding the frame
-
-  // ---- round 0: load, stage the header window.
-  uint4 v[CH];
-#pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int k = c * G + gl;
-    if (k * 16 < span)
-      v[c] = ld_stream(abase + k);
-    else
-      v[c] = make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int k = c * G + gl;
-    if (k * 16 < WIN && k * 16 < span) *reinterpret_cast<uint4*>(win + k * 16) = v[c];
-  }
-  wave_sync_lds();
-
-  auto B = [&](int j) -> uint32_t {
-    return (j >= 0 && (uint32_t)j < len) ? (uint32_t)win[shift + j] : 0u;
-  };
-  auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
-  auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
-  auto N32 = [&](int j) -> uint32_t { return N16(j) | (N16(j + 2) << 16); };
-
-  oo_gpu_rx_result r;
-  r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = 0; r.l4_off = 0;
-  r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0; r.saddr_be = 0;
-  r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
-
-  // ---- ci_parse_rx_vlan (netif_event.c:116-132)
-  int pre_l3 = 14, vlan = 0;
-  if (BE16(12) == 0x8100u) {
-    pre_l3 = 18;
-    vlan = (int)(BE16(14) & 0xfffu);
-    r.flags |= OO_RX_F_VLAN;
-  }
-  r.vlan = (uint16_t)vlan;
-  const int l3 = pre_l3;
-
-  // ---- L3 gate (netif_event.c:1030-1082)
-  uint32_t reason = 0xff;  // pending
-  bool is6 = false;
-  int ip_len = 0, ihl4 = 0, ip_paylen = 0, l4 = 0;
-  uint32_t proto = 0;
-  if ((int)len < pre_l3 + 20) {
-    reason = OO_RX_R_SHORT_L2;
-  } else {
-    const uint32_t et = BE16(pre_l3 - 2);
-    if (et == 0x0800u) {
-      ip_len = (int)BE16(l3 + 2);
-      ihl4 = (int)(B(l3) & 0xfu) * 4;
-      ip_paylen = ip_len - ihl4;
-      proto = B(l3 + 9);
-      if (ip_paylen <= 0 || (int)len < pre_l3 + ip_len) reason = OO_RX_R_IP4_LEN;
-      l4 = l3 + ihl4;
-    } else if (et == 0x86ddu) {
-      is6 = true;
-      r.flags |= OO_RX_F_IP6;
-      ip_paylen = (int)BE16(l3 + 4);
-      proto = B(l3 + 6);
-      if (ip_paylen <= 0 || (int)len < pre_l3 + 40 + ip_paylen) reason = OO_RX_R_IP6_LEN;
-      l4 = l3 + 40;
-    } else {
-      reason = OO_RX_R_NOT_IP;
-    }
-    if (reason != OO_RX_R_NOT_IP) {
-      r.proto = (uint8_t)proto;
-      r.ip_paylen = (uint16_t)ip_paylen;
-    }
-  }
-
-  // ---- L4 gate (netif_event.c:1084-1127) -> which region to sum.
-  uint32_t l4_gate = 0xff;  // 0xff: pass; else a drop reason
-  bool need_l4 = false;
-  int l4_len = 0;
-  uint32_t pseudo = 0;
-  if (reason == 0xff) {
-    if (proto == 6u) {
-      const int hlen = (int)((B(l4 + 12) & 0xf0u) >> 2);
-      if (ip_paylen < 20) l4_gate = OO_RX_R_TCP_SHORT;
-      else if (hlen < 20 || ip_paylen < hlen) l4_gate = OO_RX_R_TCP_CSUM;
-      else { need_l4 = true; l4_len = ip_paylen; }
-    } else if (proto == 17u) {
-      const uint32_t udp_len = BE16(l4 + 4);
-      if (ip_paylen < 8) l4_gate = OO_RX_R_UDP_SHORT;
-      else if (udp_len < 8u || udp_len > (uint32_t)ip_paylen) l4_gate = OO_RX_R_UDP_CSUM;
-      else if (!(N16(l4 + 6) == 0u && !is6)) { need_l4 = true; l4_len = (int)udp_len; }
-    } else {
-      l4_gate = OO_RX_R_PROTO_OTHER;
-    }
-    if (need_l4) {
-      // Pseudo-header words (checksum.c:215-223, 304-305, 334-335).
-      if (is6) {
-        uint32_t a = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) a += N16(l3 + 8 + 2 * i);
-        pseudo = a + (proto == 6u ? N16(l3 + 4) + 0x0600u : N16(l4 + 4) + 0x1100u);
-      } else {
-        pseudo = N16(l3 + 12) + N16(l3 + 14) + N16(l3 + 16) + N16(l3 + 18);
-        if (proto == 6u) {
-          const uint32_t pl = (uint32_t)ip_paylen & 0xffffu;
-          pseudo += 0x0600u + (((pl & 0xffu) << 8) | (pl >> 8));
-        } else {
-          pseudo += 0x1100u + N16(l4 + 4);
-        }
-      }
-    }
-  }
-
-  // ---- Sums: IPv4 header [l3, l3+ihl4) and L4 [l4, l4+l4_len), window coords.
-  const bool need_ip = (reason == 0xff) && !is6;
-  uint32_t s3 = 0, s4 = 0;
-  if (need_ip || need_l4) {
-    const int S3 = shift + l3, E3 = need_ip ? shift + l3 + ihl4 : S3;
-    const int S4 = shift + l4, E4 = need_l4 ? shift + l4 + l4_len : S4;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int p = (c * G + gl) * 16;
-      if (p < E3) s3 += chunk_sum(v[c], p, S3, E3);
-      if (need_l4) s4 += chunk_sum(v[c], p, S4, E4);
-    }
-    if (need_l4) {
-      for (int rb = RB; rb < E4; rb += RB) {
-        uint4 w[CH];
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          const int p = rb + (c * G + gl) * 16;
-          if (p < span)
-            w[c] = ld_stream(abase + (p >> 4));
-          else
-            w[c] = make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int c = 0; c < CH; ++c)
-          s4 += chunk_sum(w[c], rb + (c * G + gl) * 16, S4, E4);
-      }
-    }
-    constexpr int W3 = G < 8 ? G : 8;
-    s3 = seg_sum<W3>(s3);
-    s3 = __shfl(s3, 0, G);
-    s4 = seg_sum<G>(s4);
-  }
-
-  if (reason == 0xff && need_ip) {
-    // IHL != 0 makes the word sum non-zero, so fold == 0xffff <=> valid.
-    if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
-  }
-  if (reason == 0xff && l4_gate != 0xff) reason = l4_gate;
-  if (reason == 0xff && need_l4) {
-    uint32_t f = fold16(s4);
-    if (shift & 1) f = ((f & 0xffu) << 8) | (f >> 8);  // RFC 1071 byte-order swap
-    if (fold16(f + pseudo) != 0xffffu)
-      reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
-  }
-
-  if (reason == 0xff) {
-    // ---- handled: handle_rx_pkt (netif_event.c:250-451)
-    r.flags |= OO_RX_F_CSUM_OK;
-    r.l4_off = (uint16_t)l4;
-    const uint32_t sport = N16(l4), dport = N16(l4 + 2);
-    r.sport_be = (uint16_t)sport;
-    r.dport_be = (uint16_t)dport;
-    uint32_t a6s[4], a6d[4];
-    if (is6) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a6s[i] = N32(l3 + 8 + 4 * i);
-        a6d[i] = N32(l3 + 24 + 4 * i);
-      }
-      r.saddr_be = a6s[0] ^ a6s[1] ^ a6s[2] ^ a6s[3];
-      r.daddr_be = a6d[0] ^ a6d[1] ^ a6d[2] ^ a6d[3];
-    } else {
-      r.saddr_be = N32(l3 + 12);
-      r.daddr_be = N32(l3 + 16);
-      const uint32_t frag = BE16(l3 + 6);
-      if ((frag & 0x3fffu) != 0 || ip_len > (int)len - pre_l3) {
-        reason = OO_RX_R_IP4_FRAG;
-      } else if (ihl4 > 20) {
-        // ci_ip_options_parse (netif_event.c:135-185), signed-char lengths.
-        int o = l3 + 20;
-        const int end = l3 + ihl4;
-        bool err = false;
-        while (B(o) != 0u && o < end && !err) {
-          const uint32_t kind = B(o);
-          if (kind == 1u) {
-            ++o;
-          } else if (kind == 7u || kind == 68u || kind == 130u || kind == 136u) {
-            const int l = (int)(int8_t)(uint8_t)B(o + 1);
-            if (l < 4 || l > end - o) err = true;
-            else o += l;
-          } else {
-            err = true;
-          }
-        }
-        if (err) reason = OO_RX_R_IP4_OPTS_BAD;
-      }
-      if (reason == 0xff && proto == 6u && frag != 0x4000u && frag != 0u)
-        reason = OO_RX_R_TCP_SCATTERED;  // tcp_rx.c:4696-4699
-    }
-
-    if (reason == 0xff) {
-      // ---- demux: stage s on lane s of the group (udp_rx.c:271-306,
-      //      tcp_rx.c:4786-4835).
-      const int nst = proto == 6u ? 3 : 2;
-      Match m = {-1, 0};
-      if (is6) {
-        r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
-        if (gl < nst) {
-          uint32_t la[4], zero[4] = {0, 0, 0, 0};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) la[i] = gl == 2 ? 0u : a6d[i];
-          m = walk6(P, la, dport, gl == 0 ? a6s : zero, gl != 0, gl == 0 ? sport : 0u, proto,
-                    in.intf_i, vlan);
-        }
-      } else {
-        r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
-        if (gl < nst)
-          m = walk4(P, gl == 2 ? 0u : r.daddr_be, dport, gl == 0 ? r.saddr_be : 0u,
-                    gl == 0 ? sport : 0u, proto, in.intf_i, vlan);
-      }
-      if (proto == 17u) {
-        // ci_udp_rx_deliver's multi-destination test reads the IPv4 view of
-        // the L3 header (udp_rx.c:157-159): bytes 16..19.
-        const uint32_t d = N32(l3 + 16);
-        if ((d & 0xf0u) == 0xe0u || d == 0xffffffffu) r.flags |= OO_RX_F_MCAST;
-      }
-      const int gbase = (int)(__lane_id() & ~(uint32_t)(G - 1));
-      const uint32_t n0 = (uint32_t)__shfl((int)m.n, gbase + 0, 64);
-      const uint32_t n1 = (uint32_t)__shfl((int)m.n, gbase + 1, 64);
-      const uint32_t n2 = (uint32_t)__shfl((int)m.n, gbase + 2, 64);
-      const int32_t f0 = __shfl(m.first, gbase + 0, 64);
-      const int32_t f1 = __shfl(m.first, gbase + 1, 64);
-      const int32_t f2 = __shfl(m.first, gbase + 2, 64);
-      reason = OO_RX_R_NO_MATCH;
-      uint32_t n = 0;
-      int32_t fs = -1;
-      int stage = 0;
-      if (n0) { stage = 1; n = n0; fs = f0; }
-      else if (n1) { stage = 2; n = n1; fs = f1; }
-      else if (nst == 3 && n2) { stage = 3; n = n2; fs = f2; }
-      if (stage) {
-        reason = OO_RX_R_DELIVER;
-        r.stage = (uint8_t)stage;
-        r.sock = fs;
-        r.nmatch = (uint16_t)n;
-        if (n > 1) r.flags |= OO_RX_F_MULTI;
-      }
-    }
-  }
-  r.reason = (uint8_t)reason;
-
-  if (gl == 0 && in.active) {
-    uint4* o = reinterpret_cast<uint4*>(P.out + in.idx);
-    const uint4* src = reinterpret_cast<const uint4*>(&r);
-    o[0] = src[0];
-    o[1] = src[1];
-    atomicAdd(&lds_ctr[reason & (OO_RX_R_COUNT - 1)], 1u);
-  }
-  wave_sync_lds();  // the window is reused by the next packet
-}
-
-// ---------------------------------------------------------------------------
-
-constexpr int WAVES = 4;
-constexpr int TILE = 64;
-constexpr int SMALL_G = 4, SMALL_CH = 4;   // 256-byte window per packet
-constexpr int LARGE_G = 64, LARGE_CH = 2;  // 2 KiB per round
-constexpr int SMALL_SPAN = SMALL_G * SMALL_CH * 16;
-constexpr int NGROUPS_SMALL = 64 / SMALL_G;
-
-struct WaveLds {
-  uint4 desc[TILE];                       // 1 KiB
-  uint8_t list_small[TILE];
-  uint8_t list_large[TILE];
-  uint8_t win[NGROUPS_SMALL][WIN];        // 16 x 160 B
-};
 
 __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
   __shared__ __attribute__((aligned(16))) WaveLds lds[WAVES];
@@ -549,60 +274,293 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
   if (threadIdx.x < OO_RX_R_COUNT) ctr[threadIdx.x] = 0;
   __syncthreads();
 
-  const uint32_t ntiles = (P.n + TILE - 1) / TILE;
+  const uint32_t ntiles = (P.n + 63) / 64;
   const uint32_t stride = gridDim.x * WAVES;
   for (uint32_t tile = blockIdx.x * WAVES + wave; tile < ntiles; tile += stride) {
-    const uint32_t i = tile * TILE + lane;
-    const bool valid = i < P.n;
+    // ---- 1. descriptor (one per lane)
+    const uint32_t idx = tile * 64 + (uint32_t)lane;
+    const bool valid = idx < P.n;
     uint4 d = make_uint4(0, 0, 0, 0);
-    if (valid) d = ld_stream(reinterpret_cast<const uint4*>(P.desc) + i);
+    if (valid) d = ld_stream(reinterpret_cast<const uint4*>(P.desc) + idx);
     const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
-    uint32_t len = d.z & 0xffffu;
-    // A descriptor outside the frame buffer is treated as an empty frame.
-    if (off + len > P.frames_bytes) { len = 0; d.z &= 0xffff0000u; }
-    L.desc[lane] = d;
-    const bool small = valid && (int)((off & 15u) + len) <= SMALL_SPAN;
-    const bool large = valid && !small;
-    const uint64_t ms = __ballot(small);
-    const uint64_t ml = __ballot(large);
-    const uint32_t below_s = __builtin_amdgcn_mbcnt_hi((uint32_t)(ms >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)ms, 0));
-    const uint32_t below_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0));
-    if (small) L.list_small[below_s] = (uint8_t)lane;
-    if (large) L.list_large[below_l] = (uint8_t)lane;
-    wave_sync_lds();
-    const int ns = __popcll(ms);
-    const int nl = __popcll(ml);
+    int len = (int)(d.z & 0xffffu);
+    const int intf_i = (int)(int16_t)(d.z >> 16);
+    const bool inb = valid && off + (uint64_t)len <= P.frames_bytes;
+    if (!inb) len = 0;  // a descriptor outside the buffer is an empty frame
+    const uint64_t base = reinterpret_cast<uint64_t>(P.frames) + (inb ? off : 0);
+    const int shift = (int)(base & 15u);
+    const uint64_t abase = base - (uint64_t)shift;
+    const int span = inb ? shift + len : 0;
 
-    // SMALL: 16 packets per pass, 4 lanes each.
-    {
-      const int g = lane / SMALL_G, gl = lane % SMALL_G;
-      for (int b = 0; b < ns; b += NGROUPS_SMALL) {
-        const int j = b + g;
-        PktIn in;
-        in.active = j < ns;
-        const int li = in.active ? L.list_small[j] : 0;
-        const uint4 dd = L.desc[li];
-        in.off = in.active ? ((uint64_t)dd.x | ((uint64_t)dd.y << 32)) : 0;
-        in.len = in.active ? (dd.z & 0xffffu) : 0;
-        in.intf_i = (int16_t)(dd.z >> 16);
-        in.idx = tile * TILE + li;
-        process_packet<SMALL_G, SMALL_CH>(P, in, gl, L.win[g], ctr);
+    // ---- 2. stage the first HB window bytes of all 64 frames, transposed.
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int f = kk * 8 + (lane >> 3);
+      const int c = lane & 7;
+      const uint32_t ablo = (uint32_t)__shfl((int)(uint32_t)abase, f, 64);
+      const uint32_t abhi = (uint32_t)__shfl((int)(uint32_t)(abase >> 32), f, 64);
+      const int sp = __shfl(span, f, 64);
+      if (c * 16 < sp) {
+        const uint4* src = reinterpret_cast<const uint4*>(((uint64_t)abhi << 32) | ablo) + c;
+        *reinterpret_cast<uint4*>(&L.hdr[c][f * 16]) = ld_stream(src);
       }
     }
-    // LARGE: one wave per packet.
-    for (int j = 0; j < nl; ++j) {
-      const int li = L.list_large[j];
-      const uint4 dd = L.desc[li];
-      PktIn in;
-      in.active = true;
-      in.off = (uint64_t)dd.x | ((uint64_t)dd.y << 32);
-      in.len = dd.z & 0xffffu;
-      in.intf_i = (int16_t)(dd.z >> 16);
-      in.idx = tile * TILE + li;
-      process_packet<LARGE_G, LARGE_CH>(P, in, lane, L.win[0], ctr);
+    wave_sync_lds();
+
+    const uint8_t* my = &L.hdr[0][lane * 16];
+    auto B = [&](int j) -> uint32_t {
+      if (j < 0 || j >= len) return 0u;
+      const int w = shift + j;
+      return (uint32_t)my[(w >> 4) * ROWB + (w & 15)];
+    };
+    auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
+    auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
+    auto N32 = [&](int j) -> uint32_t { return N16(j) | (N16(j + 2) << 16); };
+
+    // ---- 3. parse (per lane)
+    uint8_t flags = 0;
+    int pre_l3 = 14, vlan = 0;
+    if (BE16(12) == 0x8100u) {  // ci_parse_rx_vlan (netif_event.c:116-132)
+      pre_l3 = 18;
+      vlan = (int)(BE16(14) & 0xfffu);
+      flags |= OO_RX_F_VLAN;
     }
+    const int l3 = pre_l3;
+    uint32_t reason = PENDING;
+    bool is6 = false, l3ok = false;
+    int ip_len = 0, ihl4 = 0, ip_paylen = 0, l4 = 0;
+    uint32_t proto = 0;
+    if (len < pre_l3 + 20) {  // netif_event.c:1030
+      reason = OO_RX_R_SHORT_L2;
+    } else {
+      const uint32_t et = BE16(pre_l3 - 2);
+      if (et == 0x0800u) {  // :1038-1058
+        l3ok = true;
+        ip_len = (int)BE16(l3 + 2);
+        ihl4 = (int)(B(l3) & 0xfu) * 4;
+        ip_paylen = ip_len - ihl4;
+        proto = B(l3 + 9);
+        if (ip_paylen <= 0 || len < pre_l3 + ip_len) reason = OO_RX_R_IP4_LEN;
+        l4 = l3 + ihl4;
+      } else if (et == 0x86ddu) {  // :1060-1076
+        l3ok = true;
+        is6 = true;
+        flags |= OO_RX_F_IP6;
+        ip_paylen = (int)BE16(l3 + 4);
+        proto = B(l3 + 6);
+        if (ip_paylen <= 0 || len < pre_l3 + 40 + ip_paylen) reason = OO_RX_R_IP6_LEN;
+        l4 = l3 + 40;
+      } else {
+        reason = OO_RX_R_NOT_IP;  // :1078
+      }
+    }
+
+    // L4 gates (netif_event.c:1084-1127) -> which region to sum.
+    uint32_t l4_gate = PENDING;
+    bool need_l4 = false;
+    int l4_len = 0;
+    uint32_t pseudo = 0;
+    if (reason == PENDING) {
+      if (proto == 6u) {
+        const int hlen = (int)((B(l4 + 12) & 0xf0u) >> 2);
+        if (ip_paylen < 20) l4_gate = OO_RX_R_TCP_SHORT;
+        else if (hlen < 20 || ip_paylen < hlen) l4_gate = OO_RX_R_TCP_CSUM;
+        else { need_l4 = true; l4_len = ip_paylen; }
+      } else if (proto == 17u) {
+        const uint32_t udp_len = BE16(l4 + 4);
+        if (ip_paylen < 8) l4_gate = OO_RX_R_UDP_SHORT;
+        else if (udp_len < 8u || udp_len > (uint32_t)ip_paylen) l4_gate = OO_RX_R_UDP_CSUM;
+        else if (!(N16(l4 + 6) == 0u && !is6)) { need_l4 = true; l4_len = (int)udp_len; }
+      } else {
+        l4_gate = OO_RX_R_PROTO_OTHER;
+      }
+      if (need_l4) {
+        // Pseudo-header words (checksum.c:215-223, 304-305, 334-335).
+        if (is6) {
+          uint32_t a = 0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) a += N16(l3 + 8 + 2 * i);
+          pseudo = a + (proto == 6u ? N16(l3 + 4) + 0x0600u : N16(l4 + 4) + 0x1100u);
+        } else {
+          pseudo = N16(l3 + 12) + N16(l3 + 14) + N16(l3 + 16) + N16(l3 + 18);
+          if (proto == 6u) {
+            const uint32_t pl = (uint32_t)ip_paylen & 0xffffu;
+            pseudo += 0x0600u + (((pl & 0xffu) << 8) | (pl >> 8));
+          } else {
+            pseudo += 0x1100u + N16(l4 + 4);
+          }
+        }
+      }
+    }
+
+    // Sums over the staged window: IPv4 header [S3,E3), L4 head [S4,min(E4,HB)).
+    const bool need_ip = reason == PENDING && !is6;
+    const int S3 = shift + l3, E3 = need_ip ? shift + l3 + ihl4 : S3;
+    const int S4 = shift + l4, E4 = need_l4 ? shift + l4 + l4_len : S4;
+    const int E4h = E4 < HB ? E4 : HB;
+    uint32_t s3 = 0, s4 = 0;
+    if (need_ip || need_l4) {
+#pragma unroll
+      for (int k = 0; k < HC; ++k) {
+        const uint4 v = *reinterpret_cast<const uint4*>(my + k * ROWB);
+        if (k * 16 < E3) s3 += chunk_sum(v, k * 16, S3, E3);
+        if (k * 16 < E4h) s4 += chunk_sum(v, k * 16, S4, E4h);
+      }
+    }
+
+    // ---- 4. stream the rest of long L4 regions with 16-lane rows.
+    const bool job = need_l4 && E4 > HB;
+    const uint64_t mj = __ballot(job);
+    if (mj != 0) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0));
+      if (job) {
+        L.jobs[below] = (uint8_t)lane;
+        L.meta[lane] = make_uint4((uint32_t)abase, (uint32_t)(abase >> 32), (uint32_t)E4, 0);
+      }
+      wave_sync_lds();
+      const int nj = __popcll(mj);
+      const int g = lane >> 4, gl = lane & 15;
+      for (int j = g; j < nj; j += 64 / SG) {
+        const int jl = L.jobs[j];
+        const uint4 mt = L.meta[jl];
+        const uint4* ab = reinterpret_cast<const uint4*>(((uint64_t)mt.y << 32) | mt.x);
+        const int e4 = (int)mt.z;
+        const int nch = (e4 + 15) >> 4;
+        uint32_t acc = 0;
+        for (int c0 = HC; c0 < nch; c0 += SG * SU) {
+          uint4 v[SU];
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const int c = c0 + gl + SG * u;
+            v[u] = c < nch ? ld_stream(ab + c) : make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const int c = c0 + gl + SG * u;
+            if (c * 16 + 16 <= e4) acc = chunk_sum_all(v[u], acc);
+            else acc += chunk_sum(v[u], c * 16, 0, e4);
+          }
+        }
+        acc = row_sum16(acc);
+        if (gl == 15) L.ssum[jl] = acc;
+      }
+      wave_sync_lds();
+      if (job) s4 += L.ssum[lane];
+    }
+
+    // ---- 5. verdict, handle_rx_pkt, demux, record (per lane).
+    if (reason == PENDING && need_ip) {
+      // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
+      if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
+    }
+    if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
+    if (reason == PENDING && need_l4) {
+      uint32_t f = fold16(s4);
+      if (shift & 1) f = ((f & 0xffu) << 8) | (f >> 8);  // RFC 1071 byte-order swap
+      if (fold16(f + pseudo) != 0xffffu)
+        reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+    }
+
+    oo_gpu_rx_result r;
+    r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
+    r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
+    r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+    if (l3ok) {
+      r.proto = (uint8_t)proto;
+      r.ip_paylen = (uint16_t)ip_paylen;
+    }
+
+    if (reason == PENDING) {
+      // handled: handle_rx_pkt (netif_event.c:250-451)
+      flags |= OO_RX_F_CSUM_OK;
+      r.l4_off = (uint16_t)l4;
+      const uint32_t sport = N16(l4), dport = N16(l4 + 2);
+      r.sport_be = (uint16_t)sport;
+      r.dport_be = (uint16_t)dport;
+      uint32_t a6s[4], a6d[4];
+      if (is6) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a6s[i] = N32(l3 + 8 + 4 * i);
+          a6d[i] = N32(l3 + 24 + 4 * i);
+        }
+        r.saddr_be = a6s[0] ^ a6s[1] ^ a6s[2] ^ a6s[3];
+        r.daddr_be = a6d[0] ^ a6d[1] ^ a6d[2] ^ a6d[3];
+      } else {
+        r.saddr_be = N32(l3 + 12);
+        r.daddr_be = N32(l3 + 16);
+        const uint32_t frag = BE16(l3 + 6);
+        if ((frag & 0x3fffu) != 0 || ip_len > len - pre_l3) {
+          reason = OO_RX_R_IP4_FRAG;  // :293-295
+        } else if (ihl4 > 20) {
+          // ci_ip_options_parse (netif_event.c:135-185), signed-char lengths.
+          int o = l3 + 20;
+          const int end = l3 + ihl4;
+          bool err = false;
+          while (B(o) != 0u && o < end && !err) {
+            const uint32_t kind = B(o);
+            if (kind == 1u) {
+              ++o;
+            } else if (kind == 7u || kind == 68u || kind == 130u || kind == 136u) {
+              const int l = (int)(int8_t)(uint8_t)B(o + 1);
+              if (l < 4 || l > end - o) err = true;
+              else o += l;
+            } else {
+              err = true;
+            }
+          }
+          if (err) reason = OO_RX_R_IP4_OPTS_BAD;
+        }
+        if (reason == PENDING && proto == 6u && frag != 0x4000u && frag != 0u)
+          reason = OO_RX_R_TCP_SCATTERED;  // tcp_rx.c:4696-4699
+      }
+
+      if (reason == PENDING) {
+        // Demux stages in reference order (udp_rx.c:271-306, tcp_rx.c:4786-4835);
+        // the first stage with a match decides.
+        r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
+        if (proto == 17u) {
+          // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
+          // of the L3 header (udp_rx.c:157-159): bytes 16..19.
+          const uint32_t dd = N32(l3 + 16);
+          if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
+        }
+        const int nst = proto == 6u ? 3 : 2;
+        Match m = {-1, 0};
+        int stage = 0;
+        for (int s = 0; s < nst && m.n == 0; ++s) {
+          if (is6) {
+            const uint32_t zero[4] = {0, 0, 0, 0};
+            m = walk6(P, s == 2 ? zero : a6d, dport, s == 0 ? a6s : zero, s != 0,
+                      s == 0 ? sport : 0u, proto, intf_i, vlan);
+          } else {
+            m = walk4(P, s == 2 ? 0u : r.daddr_be, dport, s == 0 ? r.saddr_be : 0u,
+                      s == 0 ? sport : 0u, proto, intf_i, vlan);
+          }
+          stage = s + 1;
+        }
+        reason = OO_RX_R_NO_MATCH;
+        if (m.n) {
+          reason = OO_RX_R_DELIVER;
+          r.stage = (uint8_t)stage;
+          r.sock = m.first;
+          r.nmatch = (uint16_t)m.n;
+          if (m.n > 1) flags |= OO_RX_F_MULTI;
+        }
+      }
+    }
+    r.reason = (uint8_t)reason;
+    r.flags = flags;
+
+    if (valid) {
+      uint4* o = reinterpret_cast<uint4*>(P.out + idx);
+      const uint4* src = reinterpret_cast<const uint4*>(&r);
+      o[0] = src[0];
+      o[1] = src[1];
+      atomicAdd(&ctr[reason & (OO_RX_R_COUNT - 1)], 1u);
+    }
+    wave_sync_lds();  // staging buffers are reused by the next tile
   }
 
   __syncthreads();
@@ -611,6 +569,15 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
 }
 
 }  // namespace oo_rx
+
+// Resident blocks per CU (sizes the persistent grid).
+extern "C" int oo_rx_blocks_per_cu(void) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_kernel, oo_rx::WAVES * 64, 0) !=
+      hipSuccess)
+    return 0;
+  return b;
+}
 
 // Launch wrapper used by the C-ABI layer.
 extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
