@@ -12,13 +12,13 @@ PKTGEN  := onload_amd/liboo_pktgen.so
 SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_gpu_rx.cpp
 HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 
-all: $(PRODUCT) $(PKTGEN) oracle
+all: $(PRODUCT) $(PKTGEN) oracle tools/hbm_ceiling
 
 $(PRODUCT): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
 
 $(PKTGEN): onload_amd/csrc/oo_pktgen.c onload_amd/csrc/oo_pktgen.h include/oo_gpu_rx.h
-	$(CC) $(CFLAGS) -shared -o $@ onload_amd/csrc/oo_pktgen.c
+	$(CC) $(CFLAGS) -shared -o $@ onload_amd/csrc/oo_pktgen.c -lm -lpthread
 
 oracle:
 	$(MAKE) -C oracle
@@ -33,3 +33,6 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle asm clean
+
+tools/hbm_ceiling: tools/hbm_ceiling.hip
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<

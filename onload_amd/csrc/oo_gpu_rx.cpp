@@ -27,8 +27,10 @@
 
 #include "oo_rx_device.h"
 
-extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
-extern "C" int oo_rx_blocks_per_cu(void);
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int head_grid, int tail_grid,
+                            hipStream_t stream);
+extern "C" int oo_rx_tail_groups_per_block(void);
+extern "C" int oo_rx_shape(int n_cu, oo_rx::LaunchShape* s);
 
 namespace {
 
@@ -43,6 +45,8 @@ constexpr uint32_t ST_EMPTY = 0x80000000u;
 constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
 constexpr int32_t ID6_TOMBSTONE = -1;
 constexpr int32_t ID6_EMPTY = -2;
+
+constexpr size_t kJobCtrBytes = sizeof(uint32_t) * oo_rx::JOB_SHARDS * oo_rx::JOB_CTR_STRIDE;
 
 inline bool occupied(uint32_t st) { return ((~st) & ST_EMPTY & ST_TOMBSTONE) != 0; }
 
@@ -107,7 +111,12 @@ struct oo_gpu_rx_ctx {
   Ext4* d_ip4_ext = nullptr;
   Ip6Entry* d_ip6 = nullptr;
   oo_gpu_rx_sock* d_socks = nullptr;
-  int grid_cap = 2048;
+  oo_rx::LaunchShape shape = {1024, 1024};
+  // Tail-job scratch (16 B per packet, grown on demand) and its counter
+  // (its own 16-byte block, zeroed before every batch).
+  void* d_jobs = nullptr;
+  uint64_t jobs_cap = 0;
+  uint32_t* d_njobs = nullptr;
   // host-path staging
   uint64_t stage_bytes = 0;
   uint32_t stage_pkts = 0;
@@ -279,6 +288,8 @@ void free_dev(oo_gpu_rx_ctx* c) {
   if (c->d_stage_desc) (void)hipFree(c->d_stage_desc);
   if (c->d_stage_out) (void)hipFree(c->d_stage_out);
   if (c->d_stage_ctr) (void)hipFree(c->d_stage_ctr);
+  if (c->d_jobs) (void)hipFree(c->d_jobs);
+  if (c->d_njobs) (void)hipFree(c->d_njobs);
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -346,15 +357,16 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
   {
-    // Persistent grid: exactly the resident blocks (tiles are grid-strided).
-    const int per_cu = oo_rx_blocks_per_cu();
-    c->grid_cap = prop.multiProcessorCount * (per_cu > 0 ? per_cu : 4);
+    // Persistent grids: exactly the resident blocks of each kernel.
+    oo_rx::LaunchShape sh;
+    if (oo_rx_shape(prop.multiProcessorCount, &sh) == 0) c->shape = sh;
   }
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_ip4, sizeof(Entry4) * c->ip4.size()) == hipSuccess &&
             hipMalloc(&c->d_ip4_ext, sizeof(Ext4) * c->ip4_ext.size()) == hipSuccess &&
             hipMalloc(&c->d_ip6, sizeof(Ip6Entry) * c->ip6.size()) == hipSuccess &&
-            hipMalloc(&c->d_socks, sizeof(oo_gpu_rx_sock) * c->socks.size()) == hipSuccess;
+            hipMalloc(&c->d_socks, sizeof(oo_gpu_rx_sock) * c->socks.size()) == hipSuccess &&
+            hipMalloc(&c->d_njobs, kJobCtrBytes) == hipSuccess;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
     c->stage_pkts = cfg->host_stage_pkts;
@@ -478,9 +490,27 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.socks = c->d_socks;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
   const uint32_t tiles = (n + 63) / 64;
-  const uint32_t blocks = (tiles + 3) / 4;
-  const int grid = (int)std::min<uint32_t>(blocks, (uint32_t)c->grid_cap);
-  return oo_rx_launch(&P, grid, s) == 0 ? 0 : -EIO;
+  const uint32_t hblocks = (tiles + oo_rx::HEAD_WAVES_PER_BLOCK - 1) / oo_rx::HEAD_WAVES_PER_BLOCK;
+  const int hgrid = (int)std::min<uint32_t>(hblocks, (uint32_t)c->shape.head_grid);
+  const uint32_t tgpb = (uint32_t)oo_rx_tail_groups_per_block();
+  const int tgrid = (int)std::min<uint32_t>((n + tgpb - 1) / tgpb, (uint32_t)c->shape.tail_grid);
+  const uint32_t cap = oo_rx::job_shard_cap(n, (uint32_t)hgrid);
+  const uint64_t need = (uint64_t)cap * oo_rx::JOB_SHARDS;
+  if (need > c->jobs_cap) {
+    // Grow the tail-job scratch (outside any graph capture; steady state
+    // reuses it).
+    if (hipStreamSynchronize(s) != hipSuccess) return -EIO;
+    if (c->d_jobs) (void)hipFree(c->d_jobs);
+    c->d_jobs = nullptr;
+    c->jobs_cap = 0;
+    if (hipMalloc(&c->d_jobs, need * 16) != hipSuccess) return -ENOMEM;
+    c->jobs_cap = need;
+  }
+  P.jobs = c->d_jobs;
+  P.njobs = c->d_njobs;
+  P.job_cap = cap;
+  if (hipMemsetAsync(c->d_njobs, 0, kJobCtrBytes, s) != hipSuccess) return -EIO;
+  return oo_rx_launch(&P, hgrid, tgrid, s) == 0 ? 0 : -EIO;
 }
 
 int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,

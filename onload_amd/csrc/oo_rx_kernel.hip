@@ -1,6 +1,6 @@
 // SPDX-License-Identifier: BSD-2-Clause
 //
-// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernel for Onload's software
+// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernels for Onload's software
 // receive transform: checksum verify + header parse + 4-tuple socket demux.
 //
 // Reference semantics (file:line in /root/reference):
@@ -17,31 +17,35 @@
 //   ci_netif_filter_for_each_match[_ip6]  netif_table.c:234-319, netif_table_ip6.c:110-189
 //   __onload_hash1/2/3            src/include/onload/hash.h:84-173
 //
-// Execution model (DESIGN.md "Kernel"): each wave owns tiles of 64 packets,
-// one packet per lane for everything that is per-packet and latency-bound,
-// and 16-lane rows for the byte stream:
+// Two kernels per batch (DESIGN.md "Kernels"):
 //
-//  1. one coalesced 16-B descriptor load per lane;
-//  2. header staging: the first 128 window bytes of the 64 frames are read
-//     with coalesced 16-B loads (8 lanes x 16 B per frame per instruction)
-//     and written transposed into LDS as [chunk][packet] cells, so that
-//  3. every lane parses its own packet's headers from LDS (VLAN, IPv4/IPv6
-//     gates, L4 gates, pseudo-header) and sums the IPv4 header and the part
-//     of the L4 region inside those 128 bytes;
-//  4. packets whose L4 region extends past 128 bytes are streamed by 16-lane
-//     rows (4 packets at a time per wave), 8 x 16-B loads per lane in flight,
-//     one's-complement partial sums by v_dot2_u32_u16 and a DPP row
-//     reduction (no LDS traffic);
-//  5. every lane finishes its packet: verdict, IPv4 frag/options/TCP
-//     scattered tests, the 2 or 3 filter-table lookup stages
-//     (double-hashed probe walks, all 64 lanes' walks in flight together),
-//     and one 32-byte record.
-//  Per-reason counters accumulate in LDS and are flushed once per block.
+// rx_head -- latency-bound per-packet work, one packet per lane, tiles of 64
+//   packets per wave:
+//   1. one coalesced 16-B descriptor load per lane (the next tile's is
+//      prefetched while this one is processed);
+//   2. the first 128 window bytes of the 64 frames are read with coalesced
+//      16-B loads (8 lanes x 16 B per frame per instruction) and written
+//      transposed into LDS as [chunk][packet] cells;
+//   3. every lane parses its own packet from LDS (VLAN, IPv4/IPv6 gates, L4
+//      gates, pseudo-header) and sums the IPv4 header and the part of the L4
+//      region inside the window;
+//   4. a packet whose L4 region ends inside the window gets its final
+//      verdict here; one whose region runs past it is handled
+//      speculatively as "checksum correct" and emits a 16-byte tail job;
+//   5. IPv4 frag/options/TCP-scattered tests, the 2 or 3 filter-table
+//      lookup stages (first probes of all stages issued together), and the
+//      32-byte record.
 //
-// The one's-complement verdict uses the mod-0xffff residue of the exact word
-// sum; oracle/rx_oracle.c explains why it equals the reference's
-// folded-complement test.  No MFMA: integer reduction + table probes,
-// HBM-bound.
+// rx_tail -- bandwidth-bound streaming of the long L4 regions, 16 lanes (one
+//   DPP row) per job, 8 x 16-B nontemporal loads per lane in flight, sums by
+//   v_dot2_u32_u16 and a DPP row reduction; a failed checksum rewrites the
+//   speculative record (a drop keeps only the fields a drop defines) and
+//   moves one count between the per-reason counters.
+//
+// The verdict uses the mod-0xffff residue of the exact word sum; see
+// oracle/rx_oracle.c for why that equals the reference's folded-complement
+// test, and why the sum splits into head + tail parts.  No MFMA: integer
+// reduction + table probes, HBM-bound.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -53,12 +57,13 @@ namespace oo_rx {
 typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int WAVES = 4;             // waves per block
+constexpr int HEAD_WAVES = HEAD_WAVES_PER_BLOCK;  // waves per rx_head block
+constexpr int TAIL_WAVES = 4;        // waves per rx_tail block
 constexpr int HC = 8;                // staged header chunks per packet
 constexpr int HB = HC * 16;          // staged window bytes per packet
 constexpr int ROWB = 64 * 16 + 16;   // one staged chunk of all 64 packets (+pad)
-constexpr int SG = 16;               // lanes per streaming group (one DPP row)
-constexpr int SU = 8;                // 16-B chunks per lane per streaming round
+constexpr int SG = 16;               // lanes per tail job (one DPP row)
+constexpr int SU = 8;                // 16-B chunks per lane per tail round
 
 // Filter-table entry states (netif_table.c:34-42).
 constexpr uint32_t ST_MASK = 0xc0000000u;
@@ -68,13 +73,6 @@ constexpr uint32_t ST_EMPTY = 0x80000000u;
 constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
 constexpr int ID6_EMPTY = -2;
 constexpr uint32_t PENDING = 0xffu;
-
-struct WaveLds {
-  uint8_t hdr[HC][ROWB];  // staged headers, [chunk][packet] 16-B cells
-  uint4 meta[64];         // streaming job: {abase lo, abase hi, E4, -}
-  uint32_t ssum[64];      // streamed L4 partial sums
-  uint8_t jobs[64];       // streaming job list (lane ids)
-};
 
 __device__ __forceinline__ uint4 ld_stream(const uint4* p) {
   const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
@@ -108,6 +106,9 @@ __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   s = (s & 0xffffu) + (s >> 16);
   s = (s & 0xffffu) + (s >> 16);
   return s;
+}
+__device__ __forceinline__ uint32_t swap16(uint32_t f) {
+  return ((f & 0xffu) << 8) | (f >> 8);
 }
 
 __device__ __forceinline__ uint32_t dot(uint32_t w, uint32_t m, uint32_t acc) {
@@ -188,15 +189,14 @@ __device__ __forceinline__ oo_gpu_rx_sock load_sock(const KParams& P, uint32_t i
   return s;
 }
 
-// ci_netif_filter_for_each_match (netif_table.c:234-319).
+// ci_netif_filter_for_each_match (netif_table.c:234-319), starting from the
+// already-loaded entry e at slot h1 = hash1.
 __device__ Match walk4(const KParams& P, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
-                       uint32_t proto, int intf_i, int vlan) {
+                       uint32_t proto, int intf_i, int vlan, uint32_t h1, uint2 e) {
   Match m = {-1, 0};
   const uint32_t mask = P.ip4_mask;
-  uint32_t h1 = hash3(la, lp, ra, rp, proto) & mask;
   const uint32_t first = h1;
   const uint32_t h2 = hash2(la, lp, ra, rp, proto);
-  uint2 e = P.ip4[h1];
   bool check_lport = false;
   for (uint32_t guard = 0; guard <= mask; ++guard) {
     const uint32_t st = e.x & ST_MASK;
@@ -221,18 +221,18 @@ __device__ Match walk4(const KParams& P, uint32_t la, uint32_t lp, uint32_t ra, 
   return m;
 }
 
-// ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189).
+// ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189), starting
+// from the already-loaded entry e at slot h1.
 __device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp, const uint32_t ra[4],
-                       bool ra_null, uint32_t rp, uint32_t proto, int intf_i, int vlan) {
+                       bool ra_null, uint32_t rp, uint32_t proto, int intf_i, int vlan,
+                       uint32_t h1, Ip6Entry e) {
   Match m = {-1, 0};
   const uint32_t mask = P.ip6_mask;
   const uint32_t lx = la[0] ^ la[1] ^ la[2] ^ la[3];
   const uint32_t rx = ra_null ? 0u : (ra[0] ^ ra[1] ^ ra[2] ^ ra[3]);
-  uint32_t h1 = hash3(lx, lp, rx, rp, proto) & mask;
   const uint32_t first = h1;
   const uint32_t h2 = hash2(lx, lp, rx, rp, proto);
   for (uint32_t guard = 0; guard <= mask; ++guard) {
-    const Ip6Entry e = P.ip6[h1];
     if (e.id >= 0) {
       if ((uint32_t)e.id < P.max_socks && e.laddr[0] == la[0] && e.laddr[1] == la[1] &&
           e.laddr[2] == la[2] && e.laddr[3] == la[3]) {
@@ -258,30 +258,46 @@ __device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp, cons
     }
     h1 = (h1 + h2) & mask;
     if (h1 == first) break;
+    e = P.ip6[h1];
   }
   return m;
 }
 
 // ---------------------------------------------------------------------------
+// rx_head
 
-__global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
-  __shared__ __attribute__((aligned(16))) WaveLds lds[WAVES];
+struct HeadLds {
+  uint8_t hdr[HC][ROWB];  // staged headers, [chunk][packet] 16-B cells
+};
+
+__global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
+  __shared__ __attribute__((aligned(16))) HeadLds lds[HEAD_WAVES];
   __shared__ uint32_t ctr[OO_RX_R_COUNT];
 
   const int wave = (int)(threadIdx.x >> 6);
   const int lane = (int)(threadIdx.x & 63);
-  WaveLds& L = lds[wave];
+  HeadLds& L = lds[wave];
   if (threadIdx.x < OO_RX_R_COUNT) ctr[threadIdx.x] = 0;
   __syncthreads();
 
   const uint32_t ntiles = (P.n + 63) / 64;
-  const uint32_t stride = gridDim.x * WAVES;
-  for (uint32_t tile = blockIdx.x * WAVES + wave; tile < ntiles; tile += stride) {
-    // ---- 1. descriptor (one per lane)
+  const uint32_t stride = gridDim.x * HEAD_WAVES;
+  uint32_t tile = blockIdx.x * HEAD_WAVES + wave;
+  uint4 dnext = make_uint4(0, 0, 0, 0);
+  if (tile < ntiles && tile * 64 + lane < P.n)
+    dnext = ld_stream(reinterpret_cast<const uint4*>(P.desc) + tile * 64 + lane);
+
+  for (; tile < ntiles; tile += stride) {
+    // ---- 1. descriptor (prefetched), and the next tile's
     const uint32_t idx = tile * 64 + (uint32_t)lane;
     const bool valid = idx < P.n;
-    uint4 d = make_uint4(0, 0, 0, 0);
-    if (valid) d = ld_stream(reinterpret_cast<const uint4*>(P.desc) + idx);
+    const uint4 d = dnext;
+    {
+      const uint32_t nidx = (tile + stride) * 64 + (uint32_t)lane;
+      dnext = make_uint4(0, 0, 0, 0);
+      if (tile + stride < ntiles && nidx < P.n)
+        dnext = ld_stream(reinterpret_cast<const uint4*>(P.desc) + nidx);
+    }
     const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
     int len = (int)(d.z & 0xffffu);
     const int intf_i = (int)(int16_t)(d.z >> 16);
@@ -308,10 +324,12 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     wave_sync_lds();
 
     const uint8_t* my = &L.hdr[0][lane * 16];
+    // Header byte j (j >= 0); bytes at or beyond the frame length read 0.
     auto B = [&](int j) -> uint32_t {
-      if (j < 0 || j >= len) return 0u;
-      const int w = shift + j;
-      return (uint32_t)my[(w >> 4) * ROWB + (w & 15)];
+      int w = shift + j;
+      w = w < HB ? w : HB - 1;
+      const uint32_t v = my[(w >> 4) * ROWB + (w & 15)];
+      return j < len ? v : 0u;
     };
     auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
     auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
@@ -407,61 +425,44 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
         if (k * 16 < E4h) s4 += chunk_sum(v, k * 16, S4, E4h);
       }
     }
+    wave_sync_lds();  // the staging cells are refilled by the next tile
 
-    // ---- 4. stream the rest of long L4 regions with 16-lane rows.
-    const bool job = need_l4 && E4 > HB;
-    const uint64_t mj = __ballot(job);
-    if (mj != 0) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-          (uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0));
-      if (job) {
-        L.jobs[below] = (uint8_t)lane;
-        L.meta[lane] = make_uint4((uint32_t)abase, (uint32_t)(abase >> 32), (uint32_t)E4, 0);
-      }
-      wave_sync_lds();
-      const int nj = __popcll(mj);
-      const int g = lane >> 4, gl = lane & 15;
-      for (int j = g; j < nj; j += 64 / SG) {
-        const int jl = L.jobs[j];
-        const uint4 mt = L.meta[jl];
-        const uint4* ab = reinterpret_cast<const uint4*>(((uint64_t)mt.y << 32) | mt.x);
-        const int e4 = (int)mt.z;
-        const int nch = (e4 + 15) >> 4;
-        uint32_t acc = 0;
-        for (int c0 = HC; c0 < nch; c0 += SG * SU) {
-          uint4 v[SU];
-#pragma unroll
-          for (int u = 0; u < SU; ++u) {
-            const int c = c0 + gl + SG * u;
-            v[u] = c < nch ? ld_stream(ab + c) : make_uint4(0, 0, 0, 0);
-          }
-#pragma unroll
-          for (int u = 0; u < SU; ++u) {
-            const int c = c0 + gl + SG * u;
-            if (c * 16 + 16 <= e4) acc = chunk_sum_all(v[u], acc);
-            else acc += chunk_sum(v[u], c * 16, 0, e4);
-          }
-        }
-        acc = row_sum16(acc);
-        if (gl == 15) L.ssum[jl] = acc;
-      }
-      wave_sync_lds();
-      if (job) s4 += L.ssum[lane];
-    }
-
-    // ---- 5. verdict, handle_rx_pkt, demux, record (per lane).
+    // ---- 4. verdict (or a tail job).
     if (reason == PENDING && need_ip) {
       // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
       if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
     }
     if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
+    bool job = false;
+    uint32_t cres = 0;
     if (reason == PENDING && need_l4) {
       uint32_t f = fold16(s4);
-      if (shift & 1) f = ((f & 0xffu) << 8) | (f >> 8);  // RFC 1071 byte-order swap
-      if (fold16(f + pseudo) != 0xffffu)
-        reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+      if (shift & 1) f = swap16(f);  // RFC 1071 byte-order swap
+      cres = fold16(f + pseudo);
+      if (E4 > HB) job = true;  // verdict pending on the tail
+      else if (cres != 0xffffu) reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+    }
+    {
+      const uint64_t mj = __ballot(job);
+      if (mj != 0) {
+        // One append per wave to this wave's job shard (64 shards, no hot
+        // counter: a single device-wide counter saturates near 88 adds/us).
+        const uint32_t shard = (blockIdx.x * HEAD_WAVES + (uint32_t)wave) % JOB_SHARDS;
+        uint32_t jbase = 0;
+        if (lane == 0) jbase = atomicAdd(&P.njobs[shard * JOB_CTR_STRIDE], (uint32_t)__popcll(mj));
+        jbase = (uint32_t)__shfl((int)jbase, 0, 64);
+        if (job) {
+          const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0));
+          uint4* J = reinterpret_cast<uint4*>(P.jobs) + (uint64_t)shard * P.job_cap + jbase + below;
+          *J = make_uint4((uint32_t)abase, (uint32_t)(abase >> 32),
+                          idx | ((uint32_t)(shift & 1) << 31),
+                          (cres << 16) | (uint32_t)(E4 - HB));
+        }
+      }
     }
 
+    // ---- 5. handle_rx_pkt, demux, record (per lane).
     oo_gpu_rx_result r;
     r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
     r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
@@ -517,8 +518,9 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
       }
 
       if (reason == PENDING) {
-        // Demux stages in reference order (udp_rx.c:271-306, tcp_rx.c:4786-4835);
-        // the first stage with a match decides.
+        // Demux stages in reference order (udp_rx.c:271-306,
+        // tcp_rx.c:4786-4835); the first stage with a match decides.  The
+        // first probe of every stage is loaded up front.
         r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
         if (proto == 17u) {
           // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
@@ -529,16 +531,45 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
         const int nst = proto == 6u ? 3 : 2;
         Match m = {-1, 0};
         int stage = 0;
-        for (int s = 0; s < nst && m.n == 0; ++s) {
-          if (is6) {
-            const uint32_t zero[4] = {0, 0, 0, 0};
-            m = walk6(P, s == 2 ? zero : a6d, dport, s == 0 ? a6s : zero, s != 0,
-                      s == 0 ? sport : 0u, proto, intf_i, vlan);
-          } else {
-            m = walk4(P, s == 2 ? 0u : r.daddr_be, dport, s == 0 ? r.saddr_be : 0u,
-                      s == 0 ? sport : 0u, proto, intf_i, vlan);
+        if (is6) {
+          const uint32_t zero[4] = {0, 0, 0, 0};
+          const uint32_t dx = r.daddr_be, sx = r.saddr_be;
+          const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & P.ip6_mask;
+          const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & P.ip6_mask;
+          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & P.ip6_mask;
+          const Ip6Entry e0 = P.ip6[h1_0];
+          const Ip6Entry e1 = P.ip6[h1_1];
+          Ip6Entry e2 = e1;
+          if (nst == 3) e2 = P.ip6[h1_2];
+          m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, e0);
+          stage = 1;
+          if (m.n == 0) {
+            m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, e1);
+            stage = 2;
           }
-          stage = s + 1;
+          if (m.n == 0 && nst == 3) {
+            m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, e2);
+            stage = 3;
+          }
+        } else {
+          const uint32_t da = r.daddr_be, sa = r.saddr_be;
+          const uint32_t h1_0 = hash3(da, dport, sa, sport, proto) & P.ip4_mask;
+          const uint32_t h1_1 = hash3(da, dport, 0u, 0u, proto) & P.ip4_mask;
+          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & P.ip4_mask;
+          const uint2 e0 = P.ip4[h1_0];
+          const uint2 e1 = P.ip4[h1_1];
+          uint2 e2 = e1;
+          if (nst == 3) e2 = P.ip4[h1_2];
+          m = walk4(P, da, dport, sa, sport, proto, intf_i, vlan, h1_0, e0);
+          stage = 1;
+          if (m.n == 0) {
+            m = walk4(P, da, dport, 0u, 0u, proto, intf_i, vlan, h1_1, e1);
+            stage = 2;
+          }
+          if (m.n == 0 && nst == 3) {
+            m = walk4(P, 0u, dport, 0u, 0u, proto, intf_i, vlan, h1_2, e2);
+            stage = 3;
+          }
         }
         reason = OO_RX_R_NO_MATCH;
         if (m.n) {
@@ -560,7 +591,6 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
       o[1] = src[1];
       atomicAdd(&ctr[reason & (OO_RX_R_COUNT - 1)], 1u);
     }
-    wave_sync_lds();  // staging buffers are reused by the next tile
   }
 
   __syncthreads();
@@ -568,19 +598,126 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     atomicAdd(&P.counters[threadIdx.x], ctr[threadIdx.x]);
 }
 
+// ---------------------------------------------------------------------------
+// rx_tail
+
+__global__ __launch_bounds__(TAIL_WAVES * 64) void rx_tail(KParams P) {
+  // Prefix over the job shards' counts: job v lives in shard s with
+  // pref[s] <= v < pref[s+1], at entry v - pref[s] of that shard.
+  __shared__ uint32_t pref[JOB_SHARDS + 1];
+  __shared__ __attribute__((aligned(16))) uint4 ring[TAIL_WAVES][SU][64];
+  if (threadIdx.x < JOB_SHARDS) {
+    const uint32_t c = __hip_atomic_load(&P.njobs[threadIdx.x * JOB_CTR_STRIDE], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < JOB_SHARDS; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+      if ((int)threadIdx.x >= o) x += y;
+    }
+    pref[threadIdx.x + 1] = x;
+    if (threadIdx.x == 0) pref[0] = 0;
+  }
+  __syncthreads();
+  const uint32_t njobs = pref[JOB_SHARDS];
+  const int wave = (int)(threadIdx.x >> 6);
+  const int lane = (int)(threadIdx.x & 63);
+  const int gl = lane & (SG - 1);
+  const uint32_t group = (blockIdx.x * TAIL_WAVES + (uint32_t)wave) * (64 / SG) +
+                         (uint32_t)(lane / SG);
+  const uint32_t stride = gridDim.x * TAIL_WAVES * (64 / SG);
+  const uint4* jobs = reinterpret_cast<const uint4*>(P.jobs);
+
+  auto load_job = [&](uint32_t v) -> uint4 {
+    uint32_t sh = 0;
+#pragma unroll
+    for (uint32_t step = JOB_SHARDS / 2; step; step >>= 1)
+      if (pref[sh + step] <= v) sh += step;
+    return jobs[(uint64_t)sh * P.job_cap + (v - pref[sh])];
+  };
+  uint4 jnext = group < njobs ? load_job(group) : make_uint4(0, 0, 0, 0);
+  for (uint32_t j = group; j < njobs; j += stride) {
+    // This round's job descriptor was loaded during the previous round;
+    // fetch the next one now so no round starts on a dependent load.
+    const uint4 jb = jnext;
+    if (j + stride < njobs) jnext = load_job(j + stride);
+    const uint4* ab = reinterpret_cast<const uint4*>(((uint64_t)jb.y << 32) | jb.x);
+    const int e4 = (int)(jb.w & 0xffffu) + HB;  // window end of the L4 region
+    const int nch = (e4 + 15) >> 4;
+    uint32_t acc = 0;
+    for (int c0 = HC; c0 < nch; c0 += SG * SU) {
+      // LDS-DMA (global_load_lds_dwordx4, nontemporal): lane l's 16 bytes
+      // land in cell l of ring slot u; the lane reads its own cell back.
+      // Cells of chunks past the region are never loaded and sum to 0.
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int c = c0 + gl + SG * u;
+        if (c < nch)
+          __builtin_amdgcn_global_load_lds(
+              (const void*)(ab + c), (void __attribute__((address_space(3)))*)&ring[wave][u][0], 16,
+              0, 2 /* nt */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int c = c0 + gl + SG * u;
+        const uint4 v = ring[wave][u][lane];
+        if (c * 16 + 16 <= e4) acc = chunk_sum_all(v, acc);
+        else acc += chunk_sum(v, c * 16, 0, e4);
+      }
+      __builtin_amdgcn_wave_barrier();  // the ring is refilled next round
+    }
+    acc = row_sum16(acc);
+    if (gl == SG - 1) {
+      uint32_t f = fold16(acc);
+      if (jb.z >> 31) f = swap16(f);
+      if (fold16(f + (jb.w >> 16)) != 0xffffu) {
+        // Checksum failed: the speculative record becomes a drop, which keeps
+        // only vlan, the VLAN/IP6 flags, proto and ip_paylen.
+        const uint32_t idx = jb.z & 0x7fffffffu;
+        uint4* o = reinterpret_cast<uint4*>(P.out + idx);
+        const uint4 w0 = o[0];
+        const uint32_t old_reason = w0.x & 0xffu;
+        const uint32_t proto = (w0.x >> 24) & 0xffu;
+        const uint32_t nr = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+        const uint32_t fl = (w0.x >> 8) & (OO_RX_F_VLAN | OO_RX_F_IP6);
+        o[0] = make_uint4(nr | (fl << 8) | (proto << 24), w0.y & 0xffffu,  // vlan
+                          w0.z & 0xffffu,                                    // ip_paylen
+                          0);
+        o[1] = make_uint4(0, 0, 0xffffffffu, 0);                             // sock = -1
+        if (P.counters != nullptr) {
+          atomicSub(&P.counters[old_reason & (OO_RX_R_COUNT - 1)], 1u);
+          atomicAdd(&P.counters[nr], 1u);
+        }
+      }
+    }
+  }
+}
+
 }  // namespace oo_rx
 
-// Resident blocks per CU (sizes the persistent grid).
-extern "C" int oo_rx_blocks_per_cu(void) {
-  int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_kernel, oo_rx::WAVES * 64, 0) !=
-      hipSuccess)
-    return 0;
-  return b;
+// Resident blocks per CU of each kernel (sizes the persistent grids).
+extern "C" int oo_rx_shape(int n_cu, oo_rx::LaunchShape* s) {
+  int h = 0, t = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&h, oo_rx::rx_head, oo_rx::HEAD_WAVES * 64,
+                                                   0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&t, oo_rx::rx_tail, oo_rx::TAIL_WAVES * 64,
+                                                   0) != hipSuccess)
+    return -1;
+  s->head_grid = n_cu * (h > 0 ? h : 1);
+  s->tail_grid = n_cu * (t > 0 ? t : 1);
+  return 0;
 }
 
-// Launch wrapper used by the C-ABI layer.
-extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
+// Launch both kernels of one batch on `stream` (the job-shard counters
+// must be zeroed on the stream before).
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int head_grid, int tail_grid,
+                            hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::rx_head, dim3(head_grid), dim3(oo_rx::HEAD_WAVES * 64), 0, stream,
+                     *P);
+  hipLaunchKernelGGL(oo_rx::rx_tail, dim3(tail_grid), dim3(oo_rx::TAIL_WAVES * 64), 0, stream,
+                     *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+extern "C" int oo_rx_tail_groups_per_block(void) { return oo_rx::TAIL_WAVES * (64 / oo_rx::SG); }
