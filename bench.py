@@ -57,6 +57,8 @@ def main() -> None:
     ap.add_argument("--n", type=int, default=0, help="packets per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scatter", action="store_true",
+                    help="N>1: also time an RCCL scatter of every shard from rank 0's GPU")
     ap.add_argument("--host-path", action="store_true",
                     help="also time pinned H2D + transform + D2H (printed to stderr)")
     args = ap.parse_args()
@@ -80,7 +82,9 @@ def main() -> None:
     seed = pktgen.default_seed(cfg)
     t0 = time.time()
     filters, socks = pktgen.world(cfg)
-    buf, desc = pktgen.generate(cfg, n, seed=seed, first=rank * n)
+    from shard import shard_range
+    first, _ = shard_range(n * world, rank, world)  # weak scaling: n per rank
+    buf, desc = pktgen.generate(cfg, n, seed=seed, first=first)
     log(f"[rank {rank}] generated {n} frames ({buf.nbytes / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
 
     stack = GpuRxStack(device=local)
@@ -148,6 +152,12 @@ def main() -> None:
         except Exception:
             traffic = None
 
+    scatter = None
+    if args.scatter and world > 1:
+        scatter = time_scatter(torch, dist, cfg, seed, n, rank, world, dev, buf)
+        if rank == 0:
+            log(f"[rank 0] rccl scatter: {json.dumps(scatter)}")
+
     host_path = None
     if args.host_path:
         host_path = time_host_path(torch, stack, buf, desc, dev)
@@ -185,10 +195,49 @@ def main() -> None:
         }
         if host_path is not None:
             line["host_path"] = host_path
+        if scatter is not None:
+            line["rccl_scatter"] = scatter
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_scatter(torch, dist, cfg, seed, n, rank, world, dev, my_buf, reps: int = 3):
+    """Frames of all shards start on rank 0's GPU and are scattered over
+    RCCL/xGMI (one 16-B-padded slab per rank); timed on its own, outside the
+    device-resident metric.  Each rank checks it received its own shard."""
+    from onload_amd import pktgen
+    from shard import shard_range
+    size = torch.tensor([my_buf.nbytes], dtype=torch.int64, device=dev)
+    dist.all_reduce(size, op=dist.ReduceOp.MAX)
+    slab = int(size.item() + 15) // 16 * 16
+    recv = torch.empty(slab, dtype=torch.uint8, device=dev)
+    send = None
+    if rank == 0:
+        send = []
+        for r in range(world):
+            first, _ = shard_range(n * world, r, world)
+            b, _ = pktgen.generate(cfg, n, seed=seed, first=first)
+            t = torch.zeros(slab, dtype=torch.uint8, device=dev)
+            t[: b.nbytes] = torch.from_numpy(b).to(dev)
+            send.append(t)
+    times = []
+    for r in range(reps + 1):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        dist.scatter(recv, send if rank == 0 else None, src=0)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        if r:
+            times.append(time.perf_counter() - t0)
+    ok = bool(torch.equal(recv[: my_buf.nbytes].cpu(), torch.from_numpy(my_buf)))
+    okt = torch.tensor([1 if ok else 0], device=dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    s = float(np.median(times))
+    return {"ms": round(s * 1e3, 3), "bytes_per_peer": slab,
+            "GBps_from_root": round(slab * (world - 1) / s / 1e9, 1), "verified": bool(okt.item())}
 
 
 def time_host_path(torch, stack, buf, desc, dev, reps: int = 5):

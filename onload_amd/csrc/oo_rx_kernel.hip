@@ -709,14 +709,15 @@ extern "C" int oo_rx_shape(int n_cu, oo_rx::LaunchShape* s) {
   return 0;
 }
 
-// Launch both kernels of one batch on `stream` (the job-shard counters
-// must be zeroed on the stream before).
-extern "C" int oo_rx_launch(const oo_rx::KParams* P, int head_grid, int tail_grid,
-                            hipStream_t stream) {
-  hipLaunchKernelGGL(oo_rx::rx_head, dim3(head_grid), dim3(oo_rx::HEAD_WAVES * 64), 0, stream,
-                     *P);
-  hipLaunchKernelGGL(oo_rx::rx_tail, dim3(tail_grid), dim3(oo_rx::TAIL_WAVES * 64), 0, stream,
-                     *P);
+// Launch wrappers used by the C-ABI layer (oo_gpu_rx.cpp): the head, then
+// (after the head, on the same or an event-chained stream) the tail.  The
+// job-shard counters must be zeroed before the head.
+extern "C" int oo_rx_launch_head(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::rx_head, dim3(grid), dim3(oo_rx::HEAD_WAVES * 64), 0, stream, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int oo_rx_launch_tail(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::rx_tail, dim3(grid), dim3(oo_rx::TAIL_WAVES * 64), 0, stream, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
