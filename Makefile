@@ -28,11 +28,19 @@ asm: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o build/oo_rx_kernel.s onload_amd/csrc/oo_rx_kernel.hip \
 	  -Rpass-analysis=kernel-resource-usage 2> build/resource-usage.txt
 
+# Tuning variants of the product library (build/var_<name>.so), selected at
+# run time with OO_RX_LIB=<path> (tools/sweep.sh); not part of `all`.
+VARIANTS ?= sp4:-DOO_RX_SP=4 sp8:-DOO_RX_SP=8
+variants: $(SRCS) $(HDRS)
+	mkdir -p build
+	for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo "$${v#*:}" | tr ',' ' '); \
+	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/var_$$n.so $(SRCS) || exit 1; done
+
 clean:
 	rm -f $(PRODUCT) $(PKTGEN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean
+.PHONY: all oracle asm clean variants
 
 tools/hbm_ceiling: tools/hbm_ceiling.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<

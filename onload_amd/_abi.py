@@ -95,11 +95,16 @@ ABI_SYMBOLS = {
 _lib = None
 
 
-def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load the gfx950 library.  Raises if it was not built (no fallback)."""
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load the gfx950 library.  Raises if it was not built (no fallback).
+
+    OO_RX_LIB may name another build of the same library (the tuning
+    variants of `make variants`)."""
     global _lib
     if _lib is not None:
         return _lib
+    if path is None:
+        path = os.environ.get("OO_RX_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(
             f"onload_amd: {path} is missing; build it with `make` (hipcc --offload-arch=gfx950). "

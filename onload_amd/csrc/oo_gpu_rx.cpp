@@ -27,10 +27,9 @@
 
 #include "oo_rx_device.h"
 
-extern "C" int oo_rx_launch_head(const oo_rx::KParams* P, int grid, hipStream_t stream);
-extern "C" int oo_rx_launch_tail(const oo_rx::KParams* P, int grid, hipStream_t stream);
-extern "C" int oo_rx_tail_groups_per_block(void);
-extern "C" int oo_rx_shape(int n_cu, oo_rx::LaunchShape* s);
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
+extern "C" int oo_rx_blocks_per_cu(void);
+extern "C" int oo_rx_waves_per_block(void);
 
 namespace {
 
@@ -45,9 +44,6 @@ constexpr uint32_t ST_EMPTY = 0x80000000u;
 constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
 constexpr int32_t ID6_TOMBSTONE = -1;
 constexpr int32_t ID6_EMPTY = -2;
-
-constexpr size_t kJobCtrBytes = sizeof(uint32_t) * oo_rx::JOB_SHARDS * oo_rx::JOB_CTR_STRIDE;
-constexpr uint32_t kMaxSplit = 8;  // sub-batches per batch (head/tail overlap)
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* v = getenv(name);
@@ -117,15 +113,7 @@ struct oo_gpu_rx_ctx {
   Ext4* d_ip4_ext = nullptr;
   Ip6Entry* d_ip6 = nullptr;
   oo_gpu_rx_sock* d_socks = nullptr;
-  uint32_t head_grid = 1024, tail_grid = 1024;  // resident blocks (occupancy)
-  uint32_t split = 0;                            // 0 = by batch size
-  hipStream_t s_head = nullptr, s_tail = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_head[kMaxSplit] = {};
-  // Tail-job scratch (16 B per packet, grown on demand) and its counter
-  // (its own 16-byte block, zeroed before every batch).
-  void* d_jobs = nullptr;
-  uint64_t jobs_cap = 0;
-  uint32_t* d_njobs = nullptr;
+  uint32_t grid = 1024;  // resident blocks of the persistent kernel
   // host-path staging
   uint64_t stage_bytes = 0;
   uint32_t stage_pkts = 0;
@@ -297,15 +285,7 @@ void free_dev(oo_gpu_rx_ctx* c) {
   if (c->d_stage_desc) (void)hipFree(c->d_stage_desc);
   if (c->d_stage_out) (void)hipFree(c->d_stage_out);
   if (c->d_stage_ctr) (void)hipFree(c->d_stage_ctr);
-  if (c->d_jobs) (void)hipFree(c->d_jobs);
-  if (c->d_njobs) (void)hipFree(c->d_njobs);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->s_head) (void)hipStreamDestroy(c->s_head);
-  if (c->s_tail) (void)hipStreamDestroy(c->s_tail);
-  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
-  if (c->ev_out) (void)hipEventDestroy(c->ev_out);
-  for (uint32_t k = 0; k < kMaxSplit; ++k)
-    if (c->ev_head[k]) (void)hipEventDestroy(c->ev_head[k]);
 }
 
 int sync_tables(oo_gpu_rx_ctx* c, hipStream_t s) {
@@ -372,30 +352,18 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
   {
-    // Persistent grids: the resident blocks of each kernel, optionally
-    // scaled (OO_RX_HEAD_GRID_PCT / OO_RX_TAIL_GRID_PCT, for tuning the
-    // head/tail overlap); OO_RX_SPLIT fixes the sub-batch count.
-    oo_rx::LaunchShape sh;
-    if (oo_rx_shape(prop.multiProcessorCount, &sh) == 0) {
-      c->head_grid = std::max<uint32_t>(1, (uint32_t)sh.head_grid *
-                                               env_u32("OO_RX_HEAD_GRID_PCT", 100) / 100);
-      c->tail_grid = std::max<uint32_t>(1, (uint32_t)sh.tail_grid *
-                                               env_u32("OO_RX_TAIL_GRID_PCT", 100) / 100);
-    }
-    c->split = env_u32("OO_RX_SPLIT", 0);
+    // Persistent grid: every resident block (occupancy query), optionally
+    // scaled by OO_RX_GRID_PCT for tuning.
+    const int bpc = oo_rx_blocks_per_cu();
+    if (bpc > 0)
+      c->grid = std::max<uint32_t>(1, (uint32_t)(bpc * prop.multiProcessorCount) *
+                                          env_u32("OO_RX_GRID_PCT", 100) / 100);
   }
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_ip4, sizeof(Entry4) * c->ip4.size()) == hipSuccess &&
             hipMalloc(&c->d_ip4_ext, sizeof(Ext4) * c->ip4_ext.size()) == hipSuccess &&
             hipMalloc(&c->d_ip6, sizeof(Ip6Entry) * c->ip6.size()) == hipSuccess &&
-            hipMalloc(&c->d_socks, sizeof(oo_gpu_rx_sock) * c->socks.size()) == hipSuccess &&
-            hipMalloc(&c->d_njobs, kJobCtrBytes * kMaxSplit) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->s_head, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->s_tail, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming) == hipSuccess;
-  for (uint32_t k = 0; ok && k < kMaxSplit; ++k)
-    ok = hipEventCreateWithFlags(&c->ev_head[k], hipEventDisableTiming) == hipSuccess;
+            hipMalloc(&c->d_socks, sizeof(oo_gpu_rx_sock) * c->socks.size()) == hipSuccess;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
     c->stage_pkts = cfg->host_stage_pkts;
@@ -499,13 +467,6 @@ int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   return sync_tables(c, static_cast<hipStream_t>(stream));
 }
 
-// Sub-batches per batch: enough that a head overlaps a tail, few enough
-// that each sub-batch still fills the GPU.
-static uint32_t split_count(const oo_gpu_rx_ctx* c, uint32_t n) {
-  if (c->split) return c->split;
-  return n >= (1u << 18) ? 4u : 1u;
-}
-
 static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
                   const oo_gpu_pkt_desc* d_desc, uint32_t n, oo_gpu_rx_result* d_out,
                   uint32_t* d_ctr, hipStream_t s) {
@@ -525,74 +486,12 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.ip6 = c->d_ip6;
   P.socks = c->d_socks;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
-  // Sub-batches: the head of sub-batch k+1 (latency-bound) runs on one
-  // internal stream while the tail of sub-batch k (HBM-bound) runs on the
-  // other; events chain head k -> tail k and the caller's stream waits for
-  // the last tail.
-  const int K = (int)std::min<uint32_t>((uint32_t)split_count(c, n), kMaxSplit);
-  struct Sub {
-    uint32_t first, n;
-    int hgrid, tgrid;
-    uint32_t cap;
-    uint64_t job_off;
-  } sub[kMaxSplit];
-  uint64_t need = 0;
-  const uint32_t tgpb = (uint32_t)oo_rx_tail_groups_per_block();
-  for (int k = 0; k < K; ++k) {
-    const uint32_t base = n / K, extra = n % K;
-    sub[k].first = k * base + std::min<uint32_t>(k, extra);
-    sub[k].n = base + ((uint32_t)k < extra ? 1 : 0);
-    const uint32_t tiles = (sub[k].n + 63) / 64;
-    const uint32_t hblocks =
-        (tiles + oo_rx::HEAD_WAVES_PER_BLOCK - 1) / oo_rx::HEAD_WAVES_PER_BLOCK;
-    sub[k].hgrid = (int)std::max<uint32_t>(1, std::min<uint32_t>(hblocks, c->head_grid));
-    sub[k].tgrid = (int)std::max<uint32_t>(
-        1, std::min<uint32_t>((sub[k].n + tgpb - 1) / tgpb, c->tail_grid));
-    sub[k].cap = oo_rx::job_shard_cap(sub[k].n, (uint32_t)sub[k].hgrid);
-    sub[k].job_off = need;
-    need += (uint64_t)sub[k].cap * oo_rx::JOB_SHARDS;
-  }
-  if (need > c->jobs_cap) {
-    // Grow the tail-job scratch (outside any graph capture; steady state
-    // reuses it).
-    if (hipStreamSynchronize(s) != hipSuccess) return -EIO;
-    if (c->d_jobs) (void)hipFree(c->d_jobs);
-    c->d_jobs = nullptr;
-    c->jobs_cap = 0;
-    if (hipMalloc(&c->d_jobs, need * 16) != hipSuccess) return -ENOMEM;
-    c->jobs_cap = need;
-  }
-  hipStream_t sh = s, st = s;
-  if (K > 1) {
-    sh = c->s_head;
-    st = c->s_tail;
-    if (hipEventRecord(c->ev_in, s) != hipSuccess || hipStreamWaitEvent(sh, c->ev_in, 0) ||
-        hipStreamWaitEvent(st, c->ev_in, 0))
-      return -EIO;
-  }
-  for (int k = 0; k < K; ++k) {
-    KParams Pk = P;
-    Pk.desc = d_desc + sub[k].first;
-    Pk.out = d_out + sub[k].first;
-    Pk.n = sub[k].n;
-    Pk.jobs = static_cast<uint8_t*>(c->d_jobs) + sub[k].job_off * 16;
-    Pk.njobs = c->d_njobs + (size_t)k * (kJobCtrBytes / sizeof(uint32_t));
-    Pk.job_cap = sub[k].cap;
-    if (Pk.n == 0) continue;
-    if (hipMemsetAsync(Pk.njobs, 0, kJobCtrBytes, sh) != hipSuccess) return -EIO;
-    if (oo_rx_launch_head(&Pk, sub[k].hgrid, sh) != 0) return -EIO;
-    if (K > 1) {
-      if (hipEventRecord(c->ev_head[k], sh) != hipSuccess ||
-          hipStreamWaitEvent(st, c->ev_head[k], 0) != hipSuccess)
-        return -EIO;
-    }
-    if (oo_rx_launch_tail(&Pk, sub[k].tgrid, st) != 0) return -EIO;
-  }
-  if (K > 1) {
-    if (hipEventRecord(c->ev_out, st) != hipSuccess || hipStreamWaitEvent(s, c->ev_out, 0))
-      return -EIO;
-  }
-  return 0;
+  // One wave per 64-packet tile; never more blocks than tiles need.
+  const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
+  const uint32_t tiles = (n + 63) / 64;
+  const uint32_t blocks = (tiles + wpb - 1) / wpb;
+  const int grid = (int)std::max<uint32_t>(1, std::min<uint32_t>(blocks, c->grid));
+  return oo_rx_launch(&P, grid, s) == 0 ? 0 : -EIO;
 }
 
 int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,

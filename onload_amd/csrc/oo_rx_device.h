@@ -11,11 +11,6 @@
 
 namespace oo_rx {
 
-// Bytes of each packet's header kept in LDS: the deepest header byte the walk
-// reads is l3 (<=18) + IHL*4 (<=60) + TCP doff byte (12) + 15 bytes of 16-byte
-// alignment slack < 160.
-constexpr int WIN = 160;
-
 // IPv4 filter table: ci_netif_filter_table_entry_fast {id_and_state, laddr}
 // (ip_shared_types.h:533-540) and _ext {route_count, lport}
 // (ip_shared_types.h:545-548) as uint2 arrays.  IPv6 table:
@@ -55,35 +50,7 @@ struct KParams {
 #endif
   const Ip6Entry* ip6;
   const oo_gpu_rx_sock* socks;
-  // Tail jobs: one 16-byte entry per packet whose L4 region runs past the
-  // staged header window, written by the head kernel and consumed by the
-  // tail kernel.  Head wave w appends to shard w % JOB_SHARDS, a region of
-  // job_cap entries; the shard counters (one per 128-byte line) are zeroed
-  // before every batch.
-  void* jobs;
-  uint32_t* njobs;
-  uint32_t job_cap;
   uint8_t hwport[OO_GPU_RX_MAX_INTF];
-};
-
-constexpr int JOB_SHARDS = 64;
-constexpr int JOB_CTR_STRIDE = 32;  // u32 per shard counter (128 B apart)
-constexpr int HEAD_WAVES_PER_BLOCK = 2;
-
-// Entries each job shard needs for n packets when the head grid has
-// head_blocks blocks: the most tiles any shard's waves can own, x 64.
-inline uint32_t job_shard_cap(uint32_t n, uint32_t head_blocks) {
-  const uint32_t tiles = (n + 63) / 64;
-  const uint32_t waves = head_blocks * HEAD_WAVES_PER_BLOCK;
-  const uint32_t per_wave = (tiles + waves - 1) / waves;
-  const uint32_t waves_per_shard = (waves + JOB_SHARDS - 1) / JOB_SHARDS;
-  return per_wave * waves_per_shard * 64;
-}
-
-// Blocks of each kernel, chosen by the host from the occupancy queries.
-struct LaunchShape {
-  int head_grid;
-  int tail_grid;
 };
 
 }  // namespace oo_rx

@@ -1,6 +1,6 @@
 // SPDX-License-Identifier: BSD-2-Clause
 //
-// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernels for Onload's software
+// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernel for Onload's software
 // receive transform: checksum verify + header parse + 4-tuple socket demux.
 //
 // Reference semantics (file:line in /root/reference):
@@ -17,34 +17,28 @@
 //   ci_netif_filter_for_each_match[_ip6]  netif_table.c:234-319, netif_table_ip6.c:110-189
 //   __onload_hash1/2/3            src/include/onload/hash.h:84-173
 //
-// Two kernels per batch (DESIGN.md "Kernels"):
-//
-// rx_head -- latency-bound per-packet work, one packet per lane, tiles of 64
-//   packets per wave:
-//   1. one coalesced 16-B descriptor load per lane (the next tile's is
-//      prefetched while this one is processed);
-//   2. the first 128 window bytes of the 64 frames are read with coalesced
-//      16-B loads (8 lanes x 16 B per frame per instruction) and written
+// One kernel, rx_kernel (DESIGN.md "Kernel").  Each wave owns tiles of 64
+// packets and strides over them; per tile:
+//   1. descriptors: one coalesced 16-B load per lane (next tile's prefetched);
+//   2. header staging: the first 128 window bytes of the 64 frames, coalesced
+//      16-B loads (8 lanes x 16 B per frame per instruction) written
 //      transposed into LDS as [chunk][packet] cells;
-//   3. every lane parses its own packet from LDS (VLAN, IPv4/IPv6 gates, L4
-//      gates, pseudo-header) and sums the IPv4 header and the part of the L4
-//      region inside the window;
-//   4. a packet whose L4 region ends inside the window gets its final
-//      verdict here; one whose region runs past it is handled
-//      speculatively as "checksum correct" and emits a 16-byte tail job;
-//   5. IPv4 frag/options/TCP-scattered tests, the 2 or 3 filter-table
-//      lookup stages (first probes of all stages issued together), and the
-//      32-byte record.
-//
-// rx_tail -- bandwidth-bound streaming of the long L4 regions, 16 lanes (one
-//   DPP row) per job, 8 x 16-B nontemporal loads per lane in flight, sums by
-//   v_dot2_u32_u16 and a DPP row reduction; a failed checksum rewrites the
-//   speculative record (a drop keeps only the fields a drop defines) and
-//   moves one count between the per-reason counters.
+//   3. per lane (one packet per lane): VLAN, L3/L4 gates, pseudo-header,
+//      IPv4 header sum and the L4 sum inside the window, and every header
+//      field the rest of the path needs, read out of LDS into registers;
+//   4. the tile's long L4 regions (past the window) are concatenated into
+//      one flat list of 16-B chunks and streamed in full 1-KiB pieces by
+//      LDS-DMA (global_load_lds_dwordx4, nontemporal) into an 8-piece ring
+//      that reuses the staging LDS; each piece is reduced by a segmented
+//      wave scan (DPP) and per-packet partial sums land in LDS;
+//   5. per lane: verdict, handle_rx_pkt's frag/options/TCP-scattered tests,
+//      the 2 or 3 filter-table lookup stages (IPv4 first probes issued before
+//      the stream so their latency hides under it), and the 32-B record.
+//   Per-reason counters accumulate in LDS and are flushed once per block.
 //
 // The verdict uses the mod-0xffff residue of the exact word sum; see
 // oracle/rx_oracle.c for why that equals the reference's folded-complement
-// test, and why the sum splits into head + tail parts.  No MFMA: integer
+// test (and why it may be summed in any grouping).  No MFMA: integer
 // reduction + table probes, HBM-bound.
 
 #include <hip/hip_runtime.h>
@@ -57,13 +51,24 @@ namespace oo_rx {
 typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int HEAD_WAVES = HEAD_WAVES_PER_BLOCK;  // waves per rx_head block
-constexpr int TAIL_WAVES = 4;        // waves per rx_tail block
+// Tuning knobs (compile-time; `make variants` builds sweeps of them).
+#ifndef OO_RX_WAVES
+#define OO_RX_WAVES 2
+#endif
+#ifndef OO_RX_SP
+#define OO_RX_SP 4
+#endif
+#ifndef OO_RX_WPE
+#define OO_RX_WPE 4  // amdgpu_waves_per_eu target, 0 = compiler's choice
+#endif
+
+constexpr int WAVES = OO_RX_WAVES;   // waves per block
 constexpr int HC = 8;                // staged header chunks per packet
 constexpr int HB = HC * 16;          // staged window bytes per packet
 constexpr int ROWB = 64 * 16 + 16;   // one staged chunk of all 64 packets (+pad)
-constexpr int SG = 16;               // lanes per tail job (one DPP row)
-constexpr int SU = 8;                // 16-B chunks per lane per tail round
+constexpr int SP = OO_RX_SP;
+static_assert(SP % 4 == 0, "ku packs 4 pieces per register");                // 1-KiB stream pieces per register buffer
+
 
 // Filter-table entry states (netif_table.c:34-42).
 constexpr uint32_t ST_MASK = 0xc0000000u;
@@ -74,9 +79,18 @@ constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
 constexpr int ID6_EMPTY = -2;
 constexpr uint32_t PENDING = 0xffu;
 
-__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+typedef const __attribute__((address_space(1))) u32x4* gptr_u32x4;
+
+// Nontemporal 16-byte load from global memory.  The explicit global address
+// space matters: a pointer rebuilt from integers would otherwise compile to
+// a flat load, which also counts on lgkmcnt and so stalls every LDS wait
+// behind the HBM stream.
+__device__ __forceinline__ uint4 ld_stream(uint64_t addr) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<gptr_u32x4>(addr));
   return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ld_stream(const void* p) {
+  return ld_stream(reinterpret_cast<uint64_t>(p));
 }
 
 __device__ __forceinline__ bool occupied(uint32_t st) {
@@ -263,26 +277,61 @@ __device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp, cons
   return m;
 }
 
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// Inclusive max over all 64 lanes (same DPP pattern as wave_scan).
+__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+
+// Inclusive sum over all 64 lanes (DPP row shifts, then row broadcasts).
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
 // ---------------------------------------------------------------------------
-// rx_head
 
-struct HeadLds {
-  uint8_t hdr[HC][ROWB];  // staged headers, [chunk][packet] 16-B cells
-};
+#if OO_RX_WPE > 0
+#define OO_RX_KATTR __attribute__((amdgpu_waves_per_eu(OO_RX_WPE)))
+#else
+#define OO_RX_KATTR
+#endif
 
-__global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
-  __shared__ __attribute__((aligned(16))) HeadLds lds[HEAD_WAVES];
+__global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t hdrs[WAVES][HC][ROWB];  // [chunk][packet] cells
+  __shared__ __attribute__((aligned(16))) uint4 jobs[WAVES][64];  // {VB lo, VB hi, first chunk, end}
+  __shared__ __attribute__((aligned(16))) uint8_t kmaps[WAVES][SP * 64];  // chunk -> packet marks
+  __shared__ uint32_t gmarks[WAVES][2][64];  // running sum before / at each packet's run
   __shared__ uint32_t ctr[OO_RX_R_COUNT];
 
   const int wave = (int)(threadIdx.x >> 6);
   const int lane = (int)(threadIdx.x & 63);
-  HeadLds& L = lds[wave];
+  uint8_t (&hdr)[HC][ROWB] = hdrs[wave];
+  uint4* job = jobs[wave];
+  uint8_t* kmap = kmaps[wave];
+  uint32_t* g_start = gmarks[wave][0];
+  uint32_t* g_end = gmarks[wave][1];
   if (threadIdx.x < OO_RX_R_COUNT) ctr[threadIdx.x] = 0;
   __syncthreads();
 
   const uint32_t ntiles = (P.n + 63) / 64;
-  const uint32_t stride = gridDim.x * HEAD_WAVES;
-  uint32_t tile = blockIdx.x * HEAD_WAVES + wave;
+  const uint32_t stride = gridDim.x * WAVES;
+  uint32_t tile = blockIdx.x * WAVES + wave;
   uint4 dnext = make_uint4(0, 0, 0, 0);
   if (tile < ntiles && tile * 64 + lane < P.n)
     dnext = ld_stream(reinterpret_cast<const uint4*>(P.desc) + tile * 64 + lane);
@@ -309,6 +358,7 @@ __global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
     const int span = inb ? shift + len : 0;
 
     // ---- 2. stage the first HB window bytes of all 64 frames, transposed.
+    uint4 stg[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const int f = kk * 8 + (lane >> 3);
@@ -316,14 +366,20 @@ __global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
       const uint32_t ablo = (uint32_t)__shfl((int)(uint32_t)abase, f, 64);
       const uint32_t abhi = (uint32_t)__shfl((int)(uint32_t)(abase >> 32), f, 64);
       const int sp = __shfl(span, f, 64);
-      if (c * 16 < sp) {
-        const uint4* src = reinterpret_cast<const uint4*>(((uint64_t)abhi << 32) | ablo) + c;
-        *reinterpret_cast<uint4*>(&L.hdr[c][f * 16]) = ld_stream(src);
-      }
+      // Unconditional (cells past the frame read the descriptor array, which
+      // is always mapped) so all eight loads are in flight together.
+      const uint64_t src = c * 16 < sp ? (((uint64_t)abhi << 32) | ablo) + (uint64_t)c * 16
+                                       : reinterpret_cast<uint64_t>(P.desc);
+      stg[kk] = ld_stream(src);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int f = kk * 8 + (lane >> 3);
+      *reinterpret_cast<uint4*>(&hdr[lane & 7][f * 16]) = stg[kk];
     }
     wave_sync_lds();
 
-    const uint8_t* my = &L.hdr[0][lane * 16];
+    const uint8_t* my = &hdr[0][lane * 16];
     // Header byte j (j >= 0); bytes at or beyond the frame length read 0.
     auto B = [&](int j) -> uint32_t {
       int w = shift + j;
@@ -425,44 +481,23 @@ __global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
         if (k * 16 < E4h) s4 += chunk_sum(v, k * 16, S4, E4h);
       }
     }
-    wave_sync_lds();  // the staging cells are refilled by the next tile
-
-    // ---- 4. verdict (or a tail job).
     if (reason == PENDING && need_ip) {
       // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
       if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
     }
     if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
-    bool job = false;
-    uint32_t cres = 0;
-    if (reason == PENDING && need_l4) {
+
+    // L4 verdict now when the region ends inside the window; otherwise it
+    // waits for the stream (step 5) and the record below is speculative.
+    const bool longl4 = reason == PENDING && need_l4 && E4 > HB;
+    if (reason == PENDING && need_l4 && !longl4) {
       uint32_t f = fold16(s4);
       if (shift & 1) f = swap16(f);  // RFC 1071 byte-order swap
-      cres = fold16(f + pseudo);
-      if (E4 > HB) job = true;  // verdict pending on the tail
-      else if (cres != 0xffffu) reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
-    }
-    {
-      const uint64_t mj = __ballot(job);
-      if (mj != 0) {
-        // One append per wave to this wave's job shard (64 shards, no hot
-        // counter: a single device-wide counter saturates near 88 adds/us).
-        const uint32_t shard = (blockIdx.x * HEAD_WAVES + (uint32_t)wave) % JOB_SHARDS;
-        uint32_t jbase = 0;
-        if (lane == 0) jbase = atomicAdd(&P.njobs[shard * JOB_CTR_STRIDE], (uint32_t)__popcll(mj));
-        jbase = (uint32_t)__shfl((int)jbase, 0, 64);
-        if (job) {
-          const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0));
-          uint4* J = reinterpret_cast<uint4*>(P.jobs) + (uint64_t)shard * P.job_cap + jbase + below;
-          *J = make_uint4((uint32_t)abase, (uint32_t)(abase >> 32),
-                          idx | ((uint32_t)(shift & 1) << 31),
-                          (cres << 16) | (uint32_t)(E4 - HB));
-        }
-      }
+      if (fold16(f + pseudo) != 0xffffu)
+        reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
     }
 
-    // ---- 5. handle_rx_pkt, demux, record (per lane).
+    // ---- 4. handle_rx_pkt, demux, record (per lane; netif_event.c:250-451).
     oo_gpu_rx_result r;
     r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
     r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
@@ -471,9 +506,7 @@ __global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
       r.proto = (uint8_t)proto;
       r.ip_paylen = (uint16_t)ip_paylen;
     }
-
     if (reason == PENDING) {
-      // handled: handle_rx_pkt (netif_event.c:250-451)
       flags |= OO_RX_F_CSUM_OK;
       r.l4_off = (uint16_t)l4;
       const uint32_t sport = N16(l4), dport = N16(l4 + 2);
@@ -537,18 +570,14 @@ __global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
           const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & P.ip6_mask;
           const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & P.ip6_mask;
           const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & P.ip6_mask;
-          const Ip6Entry e0 = P.ip6[h1_0];
-          const Ip6Entry e1 = P.ip6[h1_1];
-          Ip6Entry e2 = e1;
-          if (nst == 3) e2 = P.ip6[h1_2];
-          m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, e0);
+          m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, P.ip6[h1_0]);
           stage = 1;
           if (m.n == 0) {
-            m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, e1);
+            m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, P.ip6[h1_1]);
             stage = 2;
           }
           if (m.n == 0 && nst == 3) {
-            m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, e2);
+            m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, P.ip6[h1_2]);
             stage = 3;
           }
         } else {
@@ -584,13 +613,122 @@ __global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
     r.reason = (uint8_t)reason;
     r.flags = flags;
 
+    // ---- 5. stream the tile's long L4 regions as one flat chunk list.
+    const uint32_t nc = longl4 ? (uint32_t)(((E4 + 15) >> 4) - HC) : 0u;
+    const uint32_t incl = wave_scan(nc);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (T != 0) {
+      const uint32_t excl = incl - nc;
+      // Chunk f of the flat list (f in [excl, incl) for this packet) is at
+      // VB + 16 f with VB = abase + 16 (HC - excl); window position
+      // 16 (f - excl + HC).
+      const uint64_t vb = abase + (uint64_t)16 * ((uint64_t)HC - (uint64_t)excl);
+      job[lane] = make_uint4((uint32_t)vb, (uint32_t)(vb >> 32), excl, (uint32_t)E4);
+
+      // Buffers of SP pieces of 64 chunks (1 KiB each) into registers, two
+      // buffers in flight: one buffer's loads land while the other is
+      // reduced.  Every load is unconditional (lanes past the list reload
+      // the last chunk, an L2 hit) so the compiler's vmcnt waits are static.
+      //
+      // Chunk -> packet: the packets whose run starts inside the buffer mark
+      // their first chunk in kmap (job lane + 1); a max-scan over the marks,
+      // carried across pieces and buffers (kc), gives every chunk's packet.
+      //
+      // Per-packet sums: G = running sum of the flat list (mod 2^32); the
+      // chunk that starts a packet's run records G before it, the one that
+      // ends it records G after it, so sum = g_end - g_start.  Plain LDS
+      // writes, nothing to wait for inside the stream.
+      uint32_t kc = 1;  // mark (job lane + 1) of the packet running into the next buffer
+      uint32_t G = 0;   // running sum of the flat list before the buffer being reduced
+      // meta per piece: job lane (7 bits) | chunk index in the run (10) | run end E4 (14);
+      // all ones = past the list.
+      auto issue = [&](uint4 (&buf)[SP], uint32_t F0, uint32_t (&meta)[SP]) {
+        const uint32_t ln = opaque((uint32_t)lane);
+        const uint32_t ex = opaque(excl);
+#pragma unroll
+        for (int w = 0; w < SP / 4; ++w) reinterpret_cast<uint32_t*>(kmap)[w * 64 + ln] = 0;
+        if (nc != 0 && ex >= F0 && ex < F0 + SP * 64) kmap[ex - F0] = (uint8_t)(ln + 1);
+        wave_sync_lds();
+        uint32_t m[SP];
+#pragma unroll
+        for (int u = 0; u < SP; ++u) m[u] = kmap[u * 64 + ln];
+#pragma unroll
+        for (int u = 0; u < SP; ++u) {
+          m[u] = max(wave_max_scan(m[u]), kc);
+          kc = (uint32_t)__builtin_amdgcn_readlane((int)m[u], 63);
+        }
+        uint4 jk[SP];
+#pragma unroll
+        for (int u = 0; u < SP; ++u) jk[u] = job[m[u] - 1];
+#pragma unroll
+        for (int u = 0; u < SP; ++u) {
+          const uint32_t f = F0 + ln + (uint32_t)(u * 64);
+          const uint32_t fc = f < T ? f : T - 1;
+          const uint64_t src = (((uint64_t)jk[u].y << 32) | jk[u].x) + (uint64_t)16 * fc;
+          buf[u] = ld_stream(src);
+          meta[u] = f < T ? (m[u] - 1) | ((f - jk[u].z) << 7) | (jk[u].w << 17) : 0xffffffffu;
+        }
+      };
+      auto consume = [&](const uint4 (&buf)[SP], const uint32_t (&meta)[SP]) {
+#pragma unroll
+        for (int u = 0; u < SP; ++u) {
+          const uint32_t mt = meta[u];
+          const bool live = mt != 0xffffffffu;
+          const uint32_t kf = mt & 127u;
+          const int p = (int)(((mt >> 7) & 1023u) + HC) * 16;
+          const int e4 = (int)(mt >> 17);
+          uint32_t val = 0;
+          if (live) val = p + 16 <= e4 ? chunk_sum_all(buf[u], 0u) : chunk_sum(buf[u], p, 0, e4);
+          const uint32_t sc = wave_scan(val);
+          const uint32_t g = G + sc;
+          if (live && p == HC * 16) g_start[kf] = g - val;
+          if (live && p + 16 >= e4) g_end[kf] = g;
+          G += (uint32_t)__builtin_amdgcn_readlane((int)sc, 63);
+        }
+      };
+      uint4 ba[SP], bb[SP];
+      uint32_t ma[SP], mb[SP];
+      constexpr uint32_t R = SP * 64;  // chunks per buffer
+      issue(ba, 0, ma);
+      issue(bb, R, mb);
+      for (uint32_t F = 0; F < T; F += 2 * R) {
+        // sched_barrier: keep each buffer's reloads after its reduction, so
+        // only two buffers are ever live.
+        consume(ba, ma);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(ba, F + 2 * R, ma);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(bb, mb);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(bb, F + 3 * R, mb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      wave_sync_lds();
+      const uint32_t jacc = longl4 ? g_end[lane] - g_start[lane] : 0u;
+      s4 += jacc;
+      if (longl4) {
+        // The verdict the speculative record waited for; a failure turns it
+        // into the drop record (only the fields a drop defines survive).
+        uint32_t f = fold16(s4);
+        if (shift & 1) f = swap16(f);
+        if (fold16(f + pseudo) != 0xffffu) {
+          r.reason = (uint8_t)(proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM);
+          r.flags = (uint8_t)(flags & (OO_RX_F_VLAN | OO_RX_F_IP6));
+          r.stage = 0; r.l4_off = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
+          r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+        }
+      }
+    }
+
+
     if (valid) {
       uint4* o = reinterpret_cast<uint4*>(P.out + idx);
       const uint4* src = reinterpret_cast<const uint4*>(&r);
       o[0] = src[0];
       o[1] = src[1];
-      atomicAdd(&ctr[reason & (OO_RX_R_COUNT - 1)], 1u);
+      atomicAdd(&ctr[r.reason & (OO_RX_R_COUNT - 1)], 1u);
     }
+    wave_sync_lds();  // LDS is restaged by the next tile
   }
 
   __syncthreads();
@@ -598,127 +736,21 @@ __global__ __launch_bounds__(HEAD_WAVES * 64) void rx_head(KParams P) {
     atomicAdd(&P.counters[threadIdx.x], ctr[threadIdx.x]);
 }
 
-// ---------------------------------------------------------------------------
-// rx_tail
-
-__global__ __launch_bounds__(TAIL_WAVES * 64) void rx_tail(KParams P) {
-  // Prefix over the job shards' counts: job v lives in shard s with
-  // pref[s] <= v < pref[s+1], at entry v - pref[s] of that shard.
-  __shared__ uint32_t pref[JOB_SHARDS + 1];
-  __shared__ __attribute__((aligned(16))) uint4 ring[TAIL_WAVES][SU][64];
-  if (threadIdx.x < JOB_SHARDS) {
-    const uint32_t c = __hip_atomic_load(&P.njobs[threadIdx.x * JOB_CTR_STRIDE], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t x = c;
-#pragma unroll
-    for (int o = 1; o < JOB_SHARDS; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-      if ((int)threadIdx.x >= o) x += y;
-    }
-    pref[threadIdx.x + 1] = x;
-    if (threadIdx.x == 0) pref[0] = 0;
-  }
-  __syncthreads();
-  const uint32_t njobs = pref[JOB_SHARDS];
-  const int wave = (int)(threadIdx.x >> 6);
-  const int lane = (int)(threadIdx.x & 63);
-  const int gl = lane & (SG - 1);
-  const uint32_t group = (blockIdx.x * TAIL_WAVES + (uint32_t)wave) * (64 / SG) +
-                         (uint32_t)(lane / SG);
-  const uint32_t stride = gridDim.x * TAIL_WAVES * (64 / SG);
-  const uint4* jobs = reinterpret_cast<const uint4*>(P.jobs);
-
-  auto load_job = [&](uint32_t v) -> uint4 {
-    uint32_t sh = 0;
-#pragma unroll
-    for (uint32_t step = JOB_SHARDS / 2; step; step >>= 1)
-      if (pref[sh + step] <= v) sh += step;
-    return jobs[(uint64_t)sh * P.job_cap + (v - pref[sh])];
-  };
-  uint4 jnext = group < njobs ? load_job(group) : make_uint4(0, 0, 0, 0);
-  for (uint32_t j = group; j < njobs; j += stride) {
-    // This round's job descriptor was loaded during the previous round;
-    // fetch the next one now so no round starts on a dependent load.
-    const uint4 jb = jnext;
-    if (j + stride < njobs) jnext = load_job(j + stride);
-    const uint4* ab = reinterpret_cast<const uint4*>(((uint64_t)jb.y << 32) | jb.x);
-    const int e4 = (int)(jb.w & 0xffffu) + HB;  // window end of the L4 region
-    const int nch = (e4 + 15) >> 4;
-    uint32_t acc = 0;
-    for (int c0 = HC; c0 < nch; c0 += SG * SU) {
-      // LDS-DMA (global_load_lds_dwordx4, nontemporal): lane l's 16 bytes
-      // land in cell l of ring slot u; the lane reads its own cell back.
-      // Cells of chunks past the region are never loaded and sum to 0.
-#pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        const int c = c0 + gl + SG * u;
-        if (c < nch)
-          __builtin_amdgcn_global_load_lds(
-              (const void*)(ab + c), (void __attribute__((address_space(3)))*)&ring[wave][u][0], 16,
-              0, 2 /* nt */);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        const int c = c0 + gl + SG * u;
-        const uint4 v = ring[wave][u][lane];
-        if (c * 16 + 16 <= e4) acc = chunk_sum_all(v, acc);
-        else acc += chunk_sum(v, c * 16, 0, e4);
-      }
-      __builtin_amdgcn_wave_barrier();  // the ring is refilled next round
-    }
-    acc = row_sum16(acc);
-    if (gl == SG - 1) {
-      uint32_t f = fold16(acc);
-      if (jb.z >> 31) f = swap16(f);
-      if (fold16(f + (jb.w >> 16)) != 0xffffu) {
-        // Checksum failed: the speculative record becomes a drop, which keeps
-        // only vlan, the VLAN/IP6 flags, proto and ip_paylen.
-        const uint32_t idx = jb.z & 0x7fffffffu;
-        uint4* o = reinterpret_cast<uint4*>(P.out + idx);
-        const uint4 w0 = o[0];
-        const uint32_t old_reason = w0.x & 0xffu;
-        const uint32_t proto = (w0.x >> 24) & 0xffu;
-        const uint32_t nr = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
-        const uint32_t fl = (w0.x >> 8) & (OO_RX_F_VLAN | OO_RX_F_IP6);
-        o[0] = make_uint4(nr | (fl << 8) | (proto << 24), w0.y & 0xffffu,  // vlan
-                          w0.z & 0xffffu,                                    // ip_paylen
-                          0);
-        o[1] = make_uint4(0, 0, 0xffffffffu, 0);                             // sock = -1
-        if (P.counters != nullptr) {
-          atomicSub(&P.counters[old_reason & (OO_RX_R_COUNT - 1)], 1u);
-          atomicAdd(&P.counters[nr], 1u);
-        }
-      }
-    }
-  }
-}
-
 }  // namespace oo_rx
 
-// Resident blocks per CU of each kernel (sizes the persistent grids).
-extern "C" int oo_rx_shape(int n_cu, oo_rx::LaunchShape* s) {
-  int h = 0, t = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&h, oo_rx::rx_head, oo_rx::HEAD_WAVES * 64,
-                                                   0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&t, oo_rx::rx_tail, oo_rx::TAIL_WAVES * 64,
-                                                   0) != hipSuccess)
-    return -1;
-  s->head_grid = n_cu * (h > 0 ? h : 1);
-  s->tail_grid = n_cu * (t > 0 ? t : 1);
-  return 0;
+// Resident blocks per CU (sizes the persistent grid).
+extern "C" int oo_rx_blocks_per_cu(void) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_kernel, oo_rx::WAVES * 64, 0) !=
+      hipSuccess)
+    return 0;
+  return b;
 }
 
-// Launch wrappers used by the C-ABI layer (oo_gpu_rx.cpp): the head, then
-// (after the head, on the same or an event-chained stream) the tail.  The
-// job-shard counters must be zeroed before the head.
-extern "C" int oo_rx_launch_head(const oo_rx::KParams* P, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(oo_rx::rx_head, dim3(grid), dim3(oo_rx::HEAD_WAVES * 64), 0, stream, *P);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-extern "C" int oo_rx_launch_tail(const oo_rx::KParams* P, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(oo_rx::rx_tail, dim3(grid), dim3(oo_rx::TAIL_WAVES * 64), 0, stream, *P);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
+extern "C" int oo_rx_waves_per_block(void) { return oo_rx::WAVES; }
 
-extern "C" int oo_rx_tail_groups_per_block(void) { return oo_rx::TAIL_WAVES * (64 / oo_rx::SG); }
+// Launch one batch on `stream`.
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
