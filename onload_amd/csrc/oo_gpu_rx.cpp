@@ -35,6 +35,8 @@ namespace {
 
 using oo_rx::Ip6Entry;
 using oo_rx::KParams;
+using oo_rx::Slot4;
+using oo_rx::Slot6;
 
 constexpr uint32_t ST_MASK = 0xc0000000u;
 constexpr uint32_t ID_MASK = 0x3fffffffu;
@@ -109,11 +111,18 @@ struct oo_gpu_rx_ctx {
   std::vector<Ip6Entry> ip6;
   std::vector<oo_gpu_rx_sock> socks;
   Dirty dirty_ip4, dirty_ip6, dirty_socks;
-  Entry4* d_ip4 = nullptr;
-  Ext4* d_ip4_ext = nullptr;
-  Ip6Entry* d_ip6 = nullptr;
-  oo_gpu_rx_sock* d_socks = nullptr;
+  // Device layout (oo_rx_device.h): slot records + not-EMPTY bitmaps, built
+  // from the mirror above at sync time.
+  std::vector<Slot4> slot4;
+  std::vector<uint32_t> occ4;
+  std::vector<Slot6> slot6;
+  std::vector<uint32_t> occ6;
+  Slot4* d_slot4 = nullptr;
+  uint32_t* d_occ4 = nullptr;
+  Slot6* d_slot6 = nullptr;
+  uint32_t* d_occ6 = nullptr;
   uint32_t grid = 1024;  // resident blocks of the persistent kernel
+  uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
   // host-path staging
   uint64_t stage_bytes = 0;
   uint32_t stage_pkts = 0;
@@ -268,19 +277,19 @@ int ip6_lookup(const oo_gpu_rx_ctx* c, const uint8_t* la, uint32_t lp, const uin
 const uint8_t kZero16[16] = {0};
 
 template <typename T>
-int upload(T* dst, const std::vector<T>& src, Dirty& d, hipStream_t s) {
-  if (!d.any()) return 0;
-  hipError_t e = hipMemcpyAsync(dst + d.lo, src.data() + d.lo, sizeof(T) * (d.hi - d.lo),
-                                hipMemcpyHostToDevice, s);
-  d.clear();
-  return e == hipSuccess ? 0 : -EIO;
+int upload(T* dst, const std::vector<T>& src, uint32_t lo, uint32_t hi, hipStream_t s) {
+  if (hi <= lo) return 0;
+  return hipMemcpyAsync(dst + lo, src.data() + lo, sizeof(T) * (hi - lo), hipMemcpyHostToDevice,
+                        s) == hipSuccess
+             ? 0
+             : -EIO;
 }
 
 void free_dev(oo_gpu_rx_ctx* c) {
-  if (c->d_ip4) (void)hipFree(c->d_ip4);
-  if (c->d_ip4_ext) (void)hipFree(c->d_ip4_ext);
-  if (c->d_ip6) (void)hipFree(c->d_ip6);
-  if (c->d_socks) (void)hipFree(c->d_socks);
+  if (c->d_slot4) (void)hipFree(c->d_slot4);
+  if (c->d_occ4) (void)hipFree(c->d_occ4);
+  if (c->d_slot6) (void)hipFree(c->d_slot6);
+  if (c->d_occ6) (void)hipFree(c->d_occ6);
   if (c->d_stage_frames) (void)hipFree(c->d_stage_frames);
   if (c->d_stage_desc) (void)hipFree(c->d_stage_desc);
   if (c->d_stage_out) (void)hipFree(c->d_stage_out);
@@ -288,18 +297,94 @@ void free_dev(oo_gpu_rx_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
+// Slot record i from the mirror: the entry, its ext entry and the fields of
+// the socket its id names (what netif_table.c:192-231 reads through the id).
+void build_slot4(oo_gpu_rx_ctx* c, uint32_t i) {
+  Slot4& r = c->slot4[i];
+  const Entry4& e = c->ip4[i];
+  memset(&r, 0, sizeof(r));
+  r.id_state = e.id_state;
+  r.laddr = e.laddr;
+  r.lport = c->ip4_ext[i].lport;
+  const uint32_t id = e.id_state & ID_MASK;
+  if ((e.id_state & ST_MASK) != ST_EMPTY && id < c->max_socks) {
+    const oo_gpu_rx_sock& k = c->socks[id];
+    r.raddr = k.raddr_be32;
+    r.rport = k.rport_be16;
+    r.proto = k.protocol;
+    r.sflags = k.flags;
+    r.b2d_vlan = k.bind2dev_vlan;
+    r.hwports = k.bind2dev_hwports;
+  }
+}
+
+void build_slot6(oo_gpu_rx_ctx* c, uint32_t i) {
+  Slot6& r = c->slot6[i];
+  const Ip6Entry& e = c->ip6[i];
+  memset(&r, 0, sizeof(r));
+  r.id = e.id;
+  memcpy(r.laddr, e.laddr, 16);
+  if (e.id >= 0 && (uint32_t)e.id < c->max_socks) {
+    const oo_gpu_rx_sock& k = c->socks[e.id];
+    memcpy(r.raddr, k.raddr6, 16);
+    r.lport = k.lport_be16;
+    r.rport = k.rport_be16;
+    r.proto = k.protocol;
+    r.sflags = k.flags;
+    r.b2d_vlan = k.bind2dev_vlan;
+    r.hwports = k.bind2dev_hwports;
+  }
+}
+
 int sync_tables(oo_gpu_rx_ctx* c, hipStream_t s) {
   if (c->device < 0) return -ENODEV;
   const bool any = c->dirty_ip4.any() || c->dirty_ip6.any() || c->dirty_socks.any();
   if (!any) return 0;
-  // The ext array shares the v4 dirty range.
-  Dirty d4 = c->dirty_ip4;
-  int rc = upload(c->d_ip4, c->ip4, c->dirty_ip4, s);
-  if (rc == 0) rc = upload(c->d_ip4_ext, c->ip4_ext, d4, s);
-  if (rc == 0) rc = upload(c->d_ip6, c->ip6, c->dirty_ip6, s);
-  if (rc == 0) rc = upload(c->d_socks, c->socks, c->dirty_socks, s);
-  // Pageable sources: make sure the copies consumed the mirror before the
-  // host can modify it again.
+  // Slots whose socket changed are rebuilt too.
+  if (c->dirty_socks.any()) {
+    const uint32_t lo = c->dirty_socks.lo, hi = c->dirty_socks.hi;
+    for (uint32_t i = 0; i <= c->ip4_mask; ++i) {
+      const uint32_t st = c->ip4[i].id_state;
+      const uint32_t id = st & ID_MASK;
+      if ((st & ST_MASK) != ST_EMPTY && id >= lo && id < hi) c->dirty_ip4.mark(i);
+    }
+    for (uint32_t i = 0; i <= c->ip6_mask; ++i) {
+      const int32_t id = c->ip6[i].id;
+      if (id >= 0 && (uint32_t)id >= lo && (uint32_t)id < hi) c->dirty_ip6.mark(i);
+    }
+    c->dirty_socks.clear();
+  }
+  int rc = 0;
+  if (c->dirty_ip4.any()) {
+    const uint32_t lo = c->dirty_ip4.lo, hi = c->dirty_ip4.hi;
+    for (uint32_t i = lo; i < hi; ++i) build_slot4(c, i);
+    const uint32_t wlo = lo >> 5, whi = ((hi - 1) >> 5) + 1;
+    for (uint32_t w = wlo; w < whi; ++w) {
+      uint32_t bits = 0;
+      for (uint32_t b = 0; b < 32; ++b)
+        if ((c->ip4[w * 32 + b].id_state & ST_MASK) != ST_EMPTY) bits |= 1u << b;
+      c->occ4[w] = bits;
+    }
+    rc = upload(c->d_slot4, c->slot4, lo, hi, s);
+    if (rc == 0) rc = upload(c->d_occ4, c->occ4, wlo, whi, s);
+    c->dirty_ip4.clear();
+  }
+  if (rc == 0 && c->dirty_ip6.any()) {
+    const uint32_t lo = c->dirty_ip6.lo, hi = c->dirty_ip6.hi;
+    for (uint32_t i = lo; i < hi; ++i) build_slot6(c, i);
+    const uint32_t wlo = lo >> 5, whi = ((hi - 1) >> 5) + 1;
+    for (uint32_t w = wlo; w < whi; ++w) {
+      uint32_t bits = 0;
+      for (uint32_t b = 0; b < 32 && w * 32 + b <= c->ip6_mask; ++b)
+        if (c->ip6[w * 32 + b].id != ID6_EMPTY) bits |= 1u << b;
+      c->occ6[w] = bits;
+    }
+    rc = upload(c->d_slot6, c->slot6, lo, hi, s);
+    if (rc == 0) rc = upload(c->d_occ6, c->occ6, wlo, whi, s);
+    c->dirty_ip6.clear();
+  }
+  // Pageable sources: make sure the copies consumed the host arrays before
+  // the host can modify them again.
   if (rc == 0 && hipStreamSynchronize(s) != hipSuccess) rc = -EIO;
   return rc;
 }
@@ -341,6 +426,12 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
     c->ip4_ext.assign(c->ip4_mask + 1, Ext4{0, 0, 0});
     c->ip6.assign(c->ip6_mask + 1, Ip6Entry{ID6_EMPTY, 0, {0, 0, 0, 0}});
     c->socks.assign(c->max_socks, oo_gpu_rx_sock{});
+    if (!host_only) {
+      c->slot4.assign(c->ip4_mask + 1, Slot4{});
+      c->occ4.assign((c->ip4_mask >> 5) + 1, 0u);
+      c->slot6.assign(c->ip6_mask + 1, Slot6{});
+      c->occ6.assign((c->ip6_mask >> 5) + 1, 0u);
+    }
   } catch (...) {
     delete c;
     return -ENOMEM;
@@ -360,10 +451,10 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
                                           env_u32("OO_RX_GRID_PCT", 100) / 100);
   }
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipMalloc(&c->d_ip4, sizeof(Entry4) * c->ip4.size()) == hipSuccess &&
-            hipMalloc(&c->d_ip4_ext, sizeof(Ext4) * c->ip4_ext.size()) == hipSuccess &&
-            hipMalloc(&c->d_ip6, sizeof(Ip6Entry) * c->ip6.size()) == hipSuccess &&
-            hipMalloc(&c->d_socks, sizeof(oo_gpu_rx_sock) * c->socks.size()) == hipSuccess;
+            hipMalloc(&c->d_slot4, sizeof(Slot4) * c->slot4.size()) == hipSuccess &&
+            hipMalloc(&c->d_occ4, sizeof(uint32_t) * c->occ4.size()) == hipSuccess &&
+            hipMalloc(&c->d_slot6, sizeof(Slot6) * c->slot6.size()) == hipSuccess &&
+            hipMalloc(&c->d_occ6, sizeof(uint32_t) * c->occ6.size()) == hipSuccess;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
     c->stage_pkts = cfg->host_stage_pkts;
@@ -379,7 +470,6 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   }
   c->dirty_ip4.all(c->ip4_mask + 1);
   c->dirty_ip6.all(c->ip6_mask + 1);
-  c->dirty_socks.all(c->max_socks);
   if (sync_tables(c, c->stream) != 0) {
     free_dev(c);
     delete c;
@@ -480,17 +570,24 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.n = n;
   P.ip4_mask = c->ip4_mask;
   P.ip6_mask = c->ip6_mask;
-  P.max_socks = c->max_socks;
-  P.ip4 = reinterpret_cast<decltype(P.ip4)>(c->d_ip4);
-  P.ip4_ext = reinterpret_cast<decltype(P.ip4_ext)>(c->d_ip4_ext);
-  P.ip6 = c->d_ip6;
-  P.socks = c->d_socks;
+  P.slot4 = c->d_slot4;
+  P.occ4 = c->d_occ4;
+  P.slot6 = c->d_slot6;
+  P.occ6 = c->d_occ6;
+  P.stamps = c->stamps;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
-  // One wave per 64-packet tile; never more blocks than tiles need.
+  // Static balanced partition: W resident waves each take k tiles of
+  // P.tile <= 64 packets, k = ceil(n / (64 W)), P.tile = ceil(n / (W k)), so
+  // no wave does more than one tile's worth of packets beyond the average
+  // (a 64-packet tiling of 2^20 packets over 2560 waves would leave 40% of
+  // the waves running a 7th tile alone).  Small batches use fewer blocks.
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
-  const uint32_t tiles = (n + 63) / 64;
-  const uint32_t blocks = (tiles + wpb - 1) / wpb;
-  const int grid = (int)std::max<uint32_t>(1, std::min<uint32_t>(blocks, c->grid));
+  const uint32_t need = (n + 63) / 64;  // waves if every tile were full
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
+  const uint64_t W = (uint64_t)blocks * wpb;
+  const uint64_t k = (n + 64 * W - 1) / (64 * W);
+  P.tile = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (n + W * k - 1) / (W * k)));
+  const int grid = (int)blocks;
   return oo_rx_launch(&P, grid, s) == 0 ? 0 : -EIO;
 }
 
@@ -541,6 +638,16 @@ int oo_gpu_rx_batch(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes,
   if (!ok || hipStreamSynchronize(s) != hipSuccess) return -EIO;
   return (int)n;
 }
+
+// Diagnostic: device buffer for per-wave phase stamps written by builds with
+// -DOO_RX_STAMPS (tools/stamps.py); ignored by the product build.
+int oo_gpu_rx_debug_stamps(oo_gpu_rx_ctx* c, void* d_buf) {
+  if (c == nullptr) return -EINVAL;
+  c->stamps = static_cast<uint64_t*>(d_buf);
+  return 0;
+}
+
+int oo_gpu_rx_debug_grid(oo_gpu_rx_ctx* c) { return c ? (int)c->grid : -EINVAL; }
 
 const char* oo_gpu_rx_reason_str(int r) {
   switch (r) {

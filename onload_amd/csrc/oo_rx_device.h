@@ -11,9 +11,7 @@
 
 namespace oo_rx {
 
-// IPv4 filter table: ci_netif_filter_table_entry_fast {id_and_state, laddr}
-// (ip_shared_types.h:533-540) and _ext {route_count, lport}
-// (ip_shared_types.h:545-548) as uint2 arrays.  IPv6 table:
+// Host mirror of the IPv6 filter table entry
 // ci_ip6_netif_filter_table_entry {id, route_count, laddr[16]}
 // (ip_shared_types.h:579-583).
 struct Ip6Entry {
@@ -26,9 +24,47 @@ static_assert(sizeof(oo_gpu_rx_sock) == 48, "socket record layout");
 static_assert(sizeof(oo_gpu_rx_result) == 32, "result record layout");
 static_assert(sizeof(oo_gpu_pkt_desc) == 16, "descriptor layout");
 
-struct uint2_ {
-  uint32_t x, y;
+// Device copy of the filter tables, laid out for the probe (DESIGN.md
+// "Filter tables in HBM").  Per visited slot the reference walk reads the
+// table entry, the ext entry (lport) and then, through the entry's id, the
+// socket's raddr/rport/protocol/bind2dev fields (netif_table.c:192-319,
+// netif_table_ip6.c:110-189).  Here each slot is one record that already
+// carries the fields of the socket its id names, rebuilt by the host mirror
+// whenever the slot or that socket changes, so a visited slot is one 32-B
+// (IPv4) or 64-B (IPv6) load.  A bitmap of the slots that are not EMPTY
+// (1 bit per slot: 8 KiB for 2^16 IPv4 slots) ends most walks -- every walk
+// ends at its first EMPTY slot -- without touching the record array.
+struct Slot4 {
+  uint32_t id_state;  // entry: id (30 bits) | state (2 bits), netif_table.c:34-42
+  uint32_t laddr;     // entry
+  uint32_t raddr;     // socket: sock_raddr_be32
+  uint16_t lport;     // ext entry
+  uint16_t rport;     // socket: sock_rport_be16
+  uint8_t proto;      // socket: sock_protocol
+  uint8_t rsvd0;
+  uint16_t sflags;    // socket: OO_GPU_RX_SOCK_*
+  int16_t b2d_vlan;   // socket: rx_bind2dev_vlan
+  uint16_t rsvd1;
+  uint64_t hwports;   // socket: rx_bind2dev_hwports
 };
+static_assert(sizeof(Slot4) == 32, "v4 slot record layout");
+
+struct Slot6 {
+  int32_t id;         // entry: >= 0 occupied, -1 tombstone, -2 empty
+  int32_t rsvd0;
+  uint32_t laddr[4];  // entry
+  uint32_t raddr[4];  // socket: sock_ip6_raddr
+  uint16_t lport;     // socket: sock_lport_be16
+  uint16_t rport;     // socket: sock_rport_be16
+  uint8_t proto;      // socket: sock_protocol
+  uint8_t rsvd1;
+  uint16_t sflags;    // socket: OO_GPU_RX_SOCK_*
+  int16_t b2d_vlan;   // socket: rx_bind2dev_vlan
+  uint16_t rsvd2;
+  uint32_t rsvd3;
+  uint64_t hwports;   // socket: rx_bind2dev_hwports
+};
+static_assert(sizeof(Slot6) == 64, "v6 slot record layout");
 
 // Kernel arguments (passed by value).
 struct KParams {
@@ -38,18 +74,14 @@ struct KParams {
   oo_gpu_rx_result* out;
   uint32_t* counters;  // OO_RX_R_COUNT u32, may be null
   uint32_t n;
+  uint32_t tile;  // packets per tile (1..64)
   uint32_t ip4_mask;
   uint32_t ip6_mask;
-  uint32_t max_socks;
-#ifdef __HIPCC__
-  const uint2* ip4;
-  const uint2* ip4_ext;
-#else
-  const uint2_* ip4;
-  const uint2_* ip4_ext;
-#endif
-  const Ip6Entry* ip6;
-  const oo_gpu_rx_sock* socks;
+  const Slot4* slot4;
+  const uint32_t* occ4;  // bit i set: IPv4 slot i is not EMPTY
+  const Slot6* slot6;
+  const uint32_t* occ6;  // bit i set: IPv6 slot i is not EMPTY
+  uint64_t* stamps;      // diagnostic builds (OO_RX_STAMPS) only; may be null
   uint8_t hwport[OO_GPU_RX_MAX_INTF];
 };
 

@@ -17,23 +17,28 @@
 //   ci_netif_filter_for_each_match[_ip6]  netif_table.c:234-319, netif_table_ip6.c:110-189
 //   __onload_hash1/2/3            src/include/onload/hash.h:84-173
 //
-// One kernel, rx_kernel (DESIGN.md "Kernel").  Each wave owns tiles of 64
-// packets and strides over them; per tile:
-//   1. descriptors: one coalesced 16-B load per lane (next tile's prefetched);
-//   2. header staging: the first 128 window bytes of the 64 frames, coalesced
-//      16-B loads (8 lanes x 16 B per frame per instruction) written
-//      transposed into LDS as [chunk][packet] cells;
-//   3. per lane (one packet per lane): VLAN, L3/L4 gates, pseudo-header,
-//      IPv4 header sum and the L4 sum inside the window, and every header
-//      field the rest of the path needs, read out of LDS into registers;
-//   4. the tile's long L4 regions (past the window) are concatenated into
-//      one flat list of 16-B chunks and streamed in full 1-KiB pieces by
-//      LDS-DMA (global_load_lds_dwordx4, nontemporal) into an 8-piece ring
-//      that reuses the staging LDS; each piece is reduced by a segmented
-//      wave scan (DPP) and per-packet partial sums land in LDS;
-//   5. per lane: verdict, handle_rx_pkt's frag/options/TCP-scattered tests,
-//      the 2 or 3 filter-table lookup stages (IPv4 first probes issued before
-//      the stream so their latency hides under it), and the 32-B record.
+// One persistent kernel, rx_kernel (DESIGN.md "Kernel").  Each wave owns
+// tiles of 64 packets (one packet per lane for parse/demux) and strides over
+// them.  Every HBM read of frame bytes and descriptors is an LDS-DMA
+// (global_load_lds_dwordx4, nontemporal) whose completion the wave counts
+// itself with `s_waitcnt vmcnt(N)`; only the filter-table probes are plain
+// loads.  Per tile:
+//   1. descriptors: one 1-KiB LDS-DMA piece (the next tile's is issued as
+//      soon as this one is read);
+//   2. header window: the first 128 bytes of each frame, 8 pieces, lane =
+//      packet, landing transposed as [chunk][packet] 16-B cells;
+//   3. body: the frame bytes past the window, streamed through a ring of R
+//      1-KiB slots.  Eight lanes (an 8-lane group, 128 contiguous bytes per
+//      round) stream one packet at a time; the tile's packets with a body are
+//      dealt round-robin to the wave's eight groups.  The first R pieces are
+//      issued before the parse, so they land while it runs;
+//   4. per lane: VLAN, L3/L4 gates, pseudo-header, window sums, handle_rx_pkt's
+//      frag/options/TCP-scattered tests, the 2 or 3 lookup stages, a
+//      speculative 32-B record;
+//   5. the body stream: every lane sums its 16-B chunk (masked at the L4
+//      region end), accumulates per packet, and an 8-lane DPP reduction hands
+//      each packet's body sum to its parse lane, which then decides the
+//      verdict the record waited for.
 //   Per-reason counters accumulate in LDS and are flushed once per block.
 //
 // The verdict uses the mod-0xffff residue of the exact word sum; see
@@ -55,20 +60,20 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef OO_RX_WAVES
 #define OO_RX_WAVES 2
 #endif
-#ifndef OO_RX_SP
-#define OO_RX_SP 4
+#ifndef OO_RX_RING
+#define OO_RX_RING 6
 #endif
 #ifndef OO_RX_WPE
-#define OO_RX_WPE 4  // amdgpu_waves_per_eu target, 0 = compiler's choice
+#define OO_RX_WPE 0  // amdgpu_waves_per_eu target, 0 = compiler's choice
 #endif
 
 constexpr int WAVES = OO_RX_WAVES;   // waves per block
+constexpr int R = OO_RX_RING;        // body ring slots (1 KiB each) per wave
 constexpr int HC = 8;                // staged header chunks per packet
 constexpr int HB = HC * 16;          // staged window bytes per packet
-constexpr int ROWB = 64 * 16 + 16;   // one staged chunk of all 64 packets (+pad)
-constexpr int SP = OO_RX_SP;
-static_assert(SP % 4 == 0, "ku packs 4 pieces per register");                // 1-KiB stream pieces per register buffer
-
+constexpr int ROWB = 64 * 16;        // one staged chunk of all 64 packets
+constexpr uint32_t M_LIVE = 1u << 16;  // body meta: chunk inside the frame
+constexpr uint32_t M_LAST = 1u << 17;  // body meta: the group's last round of the packet
 
 // Filter-table entry states (netif_table.c:34-42).
 constexpr uint32_t ST_MASK = 0xc0000000u;
@@ -76,21 +81,51 @@ constexpr uint32_t ID_MASK = 0x3fffffffu;
 constexpr uint32_t ST_PREFERRED = 0x00000000u;
 constexpr uint32_t ST_EMPTY = 0x80000000u;
 constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
-constexpr int ID6_EMPTY = -2;
 constexpr uint32_t PENDING = 0xffu;
 
-typedef const __attribute__((address_space(1))) u32x4* gptr_u32x4;
+typedef const __attribute__((address_space(1))) void* gptr;
+typedef __attribute__((address_space(3))) void* lptr;
 
-// Nontemporal 16-byte load from global memory.  The explicit global address
-// space matters: a pointer rebuilt from integers would otherwise compile to
-// a flat load, which also counts on lgkmcnt and so stalls every LDS wait
-// behind the HBM stream.
-__device__ __forceinline__ uint4 ld_stream(uint64_t addr) {
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<gptr_u32x4>(addr));
-  return make_uint4(v.x, v.y, v.z, v.w);
+// One 16-byte LDS-DMA per lane (global_load_lds_dwordx4, nontemporal): lane
+// l's bytes land at lds + 16 l (lds is wave-uniform).  The global address is
+// forced to the global address space: a pointer rebuilt from integers would
+// otherwise be a flat access.
+template <int AUX = 2>
+__device__ __forceinline__ void glds(uint64_t src, void* lds) {
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(src), (lptr)(lds), 16, 0, AUX);
 }
-__device__ __forceinline__ uint4 ld_stream(const void* p) {
-  return ld_stream(reinterpret_cast<uint64_t>(p));
+#ifndef OO_RX_HDR_AUX
+#define OO_RX_HDR_AUX 0  // header window: default policy (its lines are hit 8 times)
+#endif
+#ifndef OO_RX_BODY_AUX
+#define OO_RX_BODY_AUX 2  // body stream: nontemporal
+#endif
+
+// Wait until at most N of this wave's vector-memory operations (loads,
+// LDS-DMA and stores, which retire in issue order) are outstanding.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS reads the compiler cannot see.  While LDS-DMA is in flight hipcc waits
+// vmcnt(0) before any LDS access it cannot prove disjoint from the DMA
+// target, which would drain the ring on every read; these reads carry their
+// own lgkmcnt wait, and their ordering after the DMA is the caller's counted
+// vm_wait.
+__device__ __forceinline__ uint4 lds_read16(const void* p) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(v)
+               : "v"((uint32_t)(uintptr_t)(lptr)(p))
+               : "memory");
+  return v;
+}
+
+// Value of v in lane src (ds_bpermute: no LDS memory access, so it needs no
+// vmcnt wait).  Call with every lane active.
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
 __device__ __forceinline__ bool occupied(uint32_t st) {
@@ -168,12 +203,25 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
   return s;
 }
 
-// Inclusive sum over a 16-lane DPP row; lane 15 of the row holds the total.
-__device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+#ifdef OO_RX_STAMPS
+// Diagnostic phase stamps: stamps[((wave * 64 + iter) * 8) + phase] = realtime
+// (100 MHz) for the first 64 tiles of each wave.
+#define STAMP(ph, val)                                                                \
+  do {                                                                                \
+    if (P.stamps != nullptr && lane == 0 && it_ < 64)                                \
+      P.stamps[((size_t)gwave * 64 + it_) * 8 + (ph)] = (val);                        \
+  } while (0)
+#else
+#define STAMP(ph, val) \
+  do {                 \
+  } while (0)
+#endif
+
+// Sum over each 8-lane group (lanes 8g..8g+7); every lane of the group gets it.
+__device__ __forceinline__ uint32_t group_sum8(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
   return v;
 }
 
@@ -185,124 +233,97 @@ struct Match {
   uint32_t n;
 };
 
-__device__ __forceinline__ bool bind2dev_ok(const KParams& P, const oo_gpu_rx_sock& s,
-                                            int intf_i, int vlan) {
-  if (!(s.flags & OO_GPU_RX_SOCK_BIND2DEV)) return true;
-  const uint32_t hw =
-      (intf_i >= 0 && intf_i < OO_GPU_RX_MAX_INTF) ? P.hwport[intf_i] : 0xffu;
-  return hw < 64 && (s.bind2dev_hwports & (1ull << hw)) != 0 && s.bind2dev_vlan == vlan;
+__device__ __forceinline__ bool occ_bit(const uint32_t* occ, uint32_t i) {
+  return ((occ[i >> 5] >> (i & 31u)) & 1u) != 0;
 }
 
-__device__ __forceinline__ oo_gpu_rx_sock load_sock(const KParams& P, uint32_t id) {
-  const uint4* p = reinterpret_cast<const uint4*>(P.socks + id);
-  oo_gpu_rx_sock s;
-  uint4* d = reinterpret_cast<uint4*>(&s);
+// ci_sock_intf_check (netif_table.h:30-36) on the socket fields of a slot.
+__device__ __forceinline__ bool bind2dev_ok(const KParams& P, uint32_t sflags, uint64_t hwports,
+                                            int b2d_vlan, int intf_i, int vlan) {
+  if (!(sflags & OO_GPU_RX_SOCK_BIND2DEV)) return true;
+  const uint32_t hw =
+      (intf_i >= 0 && intf_i < OO_GPU_RX_MAX_INTF) ? P.hwport[intf_i] : 0xffu;
+  return hw < 64 && (hwports & (1ull << hw)) != 0 && b2d_vlan == vlan;
+}
+
+__device__ __forceinline__ Slot4 load_slot4(const KParams& P, uint32_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(P.slot4 + i);
+  Slot4 r;
+  uint4* d = reinterpret_cast<uint4*>(&r);
+  d[0] = p[0];
+  d[1] = p[1];
+  return r;
+}
+__device__ __forceinline__ Slot6 load_slot6(const KParams& P, uint32_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(P.slot6 + i);
+  Slot6 r;
+  uint4* d = reinterpret_cast<uint4*>(&r);
   d[0] = p[0];
   d[1] = p[1];
   d[2] = p[2];
-  return s;
+  d[3] = p[3];
+  return r;
 }
 
-// ci_netif_filter_for_each_match (netif_table.c:234-319), starting from the
-// already-loaded entry e at slot h1 = hash1.
+// ci_netif_filter_for_each_match (netif_table.c:234-319) over the slot
+// records, every match counted.  The caller has loaded the not-EMPTY bits of
+// the first slot (occ) and of the next one on the probe sequence (occ_next),
+// and the first slot's record when occ: the common walk (an EMPTY first
+// slot, or one occupied slot followed by an EMPTY one) needs no more loads.
 __device__ Match walk4(const KParams& P, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
-                       uint32_t proto, int intf_i, int vlan, uint32_t h1, uint2 e) {
+                       uint32_t proto, int intf_i, int vlan, uint32_t h1, uint32_t h2, bool occ,
+                       Slot4 rec, bool occ_next) {
   Match m = {-1, 0};
   const uint32_t mask = P.ip4_mask;
   const uint32_t first = h1;
-  const uint32_t h2 = hash2(la, lp, ra, rp, proto);
-  bool check_lport = false;
+  bool check_lport = false;  // the first slot's lport is implied (LPRP, hash.h:76-163)
   for (uint32_t guard = 0; guard <= mask; ++guard) {
-    const uint32_t st = e.x & ST_MASK;
-    if (check_lport ? occupied(st) : st == ST_PREFERRED) {
-      const uint32_t id = e.x & ID_MASK;
-      if (e.y == la && id < P.max_socks) {
-        const oo_gpu_rx_sock s = load_sock(P, id);
-        bool ok = s.raddr_be32 == ra && s.rport_be16 == rp && s.protocol == proto;
-        if (check_lport) ok = ok && (P.ip4_ext[h1].y & 0xffffu) == lp;
-        if (ok && bind2dev_ok(P, s, intf_i, vlan)) {
-          if (m.n == 0) m.first = (int32_t)id;
-          ++m.n;
-        }
-      }
+    if (!occ) break;  // an EMPTY slot ends the walk
+    const uint32_t st = rec.id_state & ST_MASK;
+    if ((check_lport ? occupied(st) : st == ST_PREFERRED) && rec.laddr == la &&
+        rec.raddr == ra && rec.rport == rp && rec.proto == proto &&
+        (!check_lport || rec.lport == lp) &&
+        bind2dev_ok(P, rec.sflags, rec.hwports, rec.b2d_vlan, intf_i, vlan)) {
+      if (m.n == 0) m.first = (int32_t)(rec.id_state & ID_MASK);
+      ++m.n;
     }
-    if (st == ST_EMPTY) break;
     h1 = (h1 + h2) & mask;
     if (h1 == first) break;
-    e = P.ip4[h1];
+    occ = guard == 0 ? occ_next : occ_bit(P.occ4, h1);
+    if (occ) rec = load_slot4(P, h1);
     check_lport = true;
   }
   return m;
 }
 
-// ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189), starting
-// from the already-loaded entry e at slot h1.
+// ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189) over the
+// slot records; same first-slot convention as walk4.
 __device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp, const uint32_t ra[4],
                        bool ra_null, uint32_t rp, uint32_t proto, int intf_i, int vlan,
-                       uint32_t h1, Ip6Entry e) {
+                       uint32_t h1, uint32_t h2, bool occ, Slot6 rec, bool occ_next) {
   Match m = {-1, 0};
   const uint32_t mask = P.ip6_mask;
-  const uint32_t lx = la[0] ^ la[1] ^ la[2] ^ la[3];
-  const uint32_t rx = ra_null ? 0u : (ra[0] ^ ra[1] ^ ra[2] ^ ra[3]);
   const uint32_t first = h1;
-  const uint32_t h2 = hash2(lx, lp, rx, rp, proto);
   for (uint32_t guard = 0; guard <= mask; ++guard) {
-    if (e.id >= 0) {
-      if ((uint32_t)e.id < P.max_socks && e.laddr[0] == la[0] && e.laddr[1] == la[1] &&
-          e.laddr[2] == la[2] && e.laddr[3] == la[3]) {
-        const oo_gpu_rx_sock s = load_sock(P, (uint32_t)e.id);
-        bool ok = s.lport_be16 == lp && s.protocol == proto;
-        if (ok) {
-          if (ra_null) {
-            ok = !(s.flags & OO_GPU_RX_SOCK_CONNECTED);
-          } else {
-            uint32_t r6[4];
-            __builtin_memcpy(r6, s.raddr6, 16);
-            ok = r6[0] == ra[0] && r6[1] == ra[1] && r6[2] == ra[2] && r6[3] == ra[3] &&
-                 s.rport_be16 == rp;
-          }
-        }
-        if (ok && bind2dev_ok(P, s, intf_i, vlan)) {
-          if (m.n == 0) m.first = e.id;
-          ++m.n;
-        }
-      }
-    } else if (e.id == ID6_EMPTY) {
-      break;
+    if (!occ) break;  // an EMPTY slot ends the walk (tombstones continue)
+    if (rec.id >= 0 && rec.laddr[0] == la[0] && rec.laddr[1] == la[1] &&
+        rec.laddr[2] == la[2] && rec.laddr[3] == la[3] && rec.lport == lp &&
+        rec.proto == proto &&
+        (ra_null ? !(rec.sflags & OO_GPU_RX_SOCK_CONNECTED)
+                 : (rec.raddr[0] == ra[0] && rec.raddr[1] == ra[1] && rec.raddr[2] == ra[2] &&
+                    rec.raddr[3] == ra[3] && rec.rport == rp)) &&
+        bind2dev_ok(P, rec.sflags, rec.hwports, rec.b2d_vlan, intf_i, vlan)) {
+      if (m.n == 0) m.first = rec.id;
+      ++m.n;
     }
     h1 = (h1 + h2) & mask;
     if (h1 == first) break;
-    e = P.ip6[h1];
+    occ = guard == 0 ? occ_next : occ_bit(P.occ6, h1);
+    if (occ) rec = load_slot6(P, h1);
   }
   return m;
 }
 
-__device__ __forceinline__ uint32_t opaque(uint32_t x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
-// Inclusive max over all 64 lanes (same DPP pattern as wave_scan).
-__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
-  return v;
-}
-
-// Inclusive sum over all 64 lanes (DPP row shifts, then row broadcasts).
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);   // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return v;
-}
 
 // ---------------------------------------------------------------------------
 
@@ -312,41 +333,60 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
 #define OO_RX_KATTR
 #endif
 
+// Per-wave LDS.  All LDS lives in one __shared__ array (a second __shared__
+// object can make hipcc wait vmcnt(0) before LDS reads while LDS-DMA is in
+// flight).
+struct WaveLds {
+  uint4 hdr[HC][64];   // header window, [chunk][packet] 16-B cells
+  uint4 ring[R][64];   // body ring: slot = one round of the eight groups
+  uint4 desc[64];      // the tile's descriptors
+};
+static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
+constexpr int WAVE_U4 = (int)(sizeof(WaveLds) / 16);
+
 __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t hdrs[WAVES][HC][ROWB];  // [chunk][packet] cells
-  __shared__ __attribute__((aligned(16))) uint4 jobs[WAVES][64];  // {VB lo, VB hi, first chunk, end}
-  __shared__ __attribute__((aligned(16))) uint8_t kmaps[WAVES][SP * 64];  // chunk -> packet marks
-  __shared__ uint32_t gmarks[WAVES][2][64];  // running sum before / at each packet's run
-  __shared__ uint32_t ctr[OO_RX_R_COUNT];
+  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES * WAVE_U4 + OO_RX_R_COUNT / 4];
 
   const int wave = (int)(threadIdx.x >> 6);
   const int lane = (int)(threadIdx.x & 63);
-  uint8_t (&hdr)[HC][ROWB] = hdrs[wave];
-  uint4* job = jobs[wave];
-  uint8_t* kmap = kmaps[wave];
-  uint32_t* g_start = gmarks[wave][0];
-  uint32_t* g_end = gmarks[wave][1];
+  const uint32_t grp = (uint32_t)lane >> 3;  // 8-lane group
+  const uint32_t gj = (uint32_t)lane & 7u;   // lane within the group
+  WaveLds& L = reinterpret_cast<WaveLds*>(smem)[wave];
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + WAVES * WAVE_U4);
   if (threadIdx.x < OO_RX_R_COUNT) ctr[threadIdx.x] = 0;
   __syncthreads();
 
-  const uint32_t ntiles = (P.n + 63) / 64;
+  // Tiles of P.tile packets (<= 64), sized by the host so that every wave
+  // gets the same number of tiles (oo_gpu_rx.cpp launch()).
+  const uint32_t TS = P.tile;
+  const uint32_t ntiles = (P.n + TS - 1) / TS;
   const uint32_t stride = gridDim.x * WAVES;
   uint32_t tile = blockIdx.x * WAVES + wave;
-  uint4 dnext = make_uint4(0, 0, 0, 0);
-  if (tile < ntiles && tile * 64 + lane < P.n)
-    dnext = ld_stream(reinterpret_cast<const uint4*>(P.desc) + tile * 64 + lane);
+  // Lanes with nothing to load read this always-mapped 16-B line instead, so
+  // every LDS-DMA instruction is issued by the whole wave and the counted
+  // waits stay static.
+  const uint64_t dummy = reinterpret_cast<uint64_t>(P.desc);
+  const uint64_t descs = reinterpret_cast<uint64_t>(P.desc);
+  auto issue_desc = [&](uint32_t t) {
+    const uint32_t i = t * TS + (uint32_t)lane;
+    glds((uint32_t)lane < TS && i < P.n ? descs + (uint64_t)i * 16 : dummy, &L.desc[0]);
+  };
+  if (tile < ntiles) issue_desc(tile);
+  vm_wait<0>();
+  const uint32_t gwave = blockIdx.x * WAVES + wave;
+  uint32_t it_ = 0;
+  (void)gwave;
+  (void)it_;
 
-  for (; tile < ntiles; tile += stride) {
-    // ---- 1. descriptor (prefetched), and the next tile's
-    const uint32_t idx = tile * 64 + (uint32_t)lane;
-    const bool valid = idx < P.n;
-    const uint4 d = dnext;
-    {
-      const uint32_t nidx = (tile + stride) * 64 + (uint32_t)lane;
-      dnext = make_uint4(0, 0, 0, 0);
-      if (tile + stride < ntiles && nidx < P.n)
-        dnext = ld_stream(reinterpret_cast<const uint4*>(P.desc) + nidx);
-    }
+  for (; tile < ntiles; tile += stride, ++it_) {
+    STAMP(0, __builtin_amdgcn_s_memrealtime());
+    STAMP(6, tile);
+    // ---- 1. descriptor (landed: every earlier wait retired it), then the
+    // next tile's.
+    const uint32_t idx = tile * TS + (uint32_t)lane;
+    const bool valid = (uint32_t)lane < TS && idx < P.n;
+    const uint4 d = lds_read16(&L.desc[lane]);
+    if (tile + stride < ntiles) issue_desc(tile + stride);
     const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
     int len = (int)(d.z & 0xffffu);
     const int intf_i = (int)(int16_t)(d.z >> 16);
@@ -356,30 +396,101 @@ __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
     const int shift = (int)(base & 15u);
     const uint64_t abase = base - (uint64_t)shift;
     const int span = inb ? shift + len : 0;
+    const int nwin = (span + 15) >> 4;  // 16-B chunks the frame touches
 
-    // ---- 2. stage the first HB window bytes of all 64 frames, transposed.
-    uint4 stg[8];
+    // ---- 2. header window: chunk k of every frame, lane = packet.
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int f = kk * 8 + (lane >> 3);
-      const int c = lane & 7;
-      const uint32_t ablo = (uint32_t)__shfl((int)(uint32_t)abase, f, 64);
-      const uint32_t abhi = (uint32_t)__shfl((int)(uint32_t)(abase >> 32), f, 64);
-      const int sp = __shfl(span, f, 64);
-      // Unconditional (cells past the frame read the descriptor array, which
-      // is always mapped) so all eight loads are in flight together.
-      const uint64_t src = c * 16 < sp ? (((uint64_t)abhi << 32) | ablo) + (uint64_t)c * 16
-                                       : reinterpret_cast<uint64_t>(P.desc);
-      stg[kk] = ld_stream(src);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int f = kk * 8 + (lane >> 3);
-      *reinterpret_cast<uint4*>(&hdr[lane & 7][f * 16]) = stg[kk];
-    }
-    wave_sync_lds();
+    for (int k = 0; k < HC; ++k) glds<OO_RX_HDR_AUX>(k < nwin ? abase + (uint64_t)k * 16 : dummy, &L.hdr[k][0]);
 
-    const uint8_t* my = &hdr[0][lane * 16];
+    // ---- 3. body jobs.  The packets with chunks past the window, in lane
+    // order, are list positions q = 0..M-1; group g takes q = g, g+8, ...
+    // Lane (g, j) holds the job at q = g + 8 j (a permutation, so every lane
+    // sends and receives exactly one value).
+    const uint32_t nb = nwin > HC ? (uint32_t)(nwin - HC) : 0u;
+    const uint64_t bm = __ballot(nb != 0);
+    const uint32_t M = (uint32_t)__popcll(bm);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    const uint32_t myq = nb != 0 ? below : M + (uint32_t)lane - below;
+    const uint32_t myslot = (myq & 7u) * 8u + (myq >> 3);  // lane holding job myq
+    const uint32_t jp = (uint32_t)__builtin_amdgcn_ds_permute((int)(myslot << 2), lane);
+    const uint64_t bbase = abase + HB;
+    const uint32_t jlo = lane_get((uint32_t)bbase, jp);
+    const uint32_t jhi = lane_get((uint32_t)(bbase >> 32), jp);
+    const uint32_t jnb = lane_get(nb, jp);  // 0 for lanes past the list
+    // Rounds of the body stream = the busiest group's.
+    const uint32_t gr = group_sum8((jnb + 7u) >> 3);
+    uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)gr, 0);
+#pragma unroll
+    for (int g = 1; g < 8; ++g) T = max(T, (uint32_t)__builtin_amdgcn_readlane((int)gr, 8 * g));
+
+    // Issue state: the group's job number ik, its packet ip, this lane's
+    // chunk ic (= 8 * round + gj) out of inb_, and the source address.
+    const uint32_t gsrc = grp * 8u;
+    uint32_t ik = 0;
+    uint32_t ip = lane_get(jp, gsrc), inb_ = lane_get(jnb, gsrc), ic = gj;
+    uint64_t iaddr = ((uint64_t)lane_get(jhi, gsrc) << 32 | lane_get(jlo, gsrc)) + gj * 16u;
+    // Per piece (slot u) and lane, meta[u] says what landed: before the
+    // parse, {packet, chunk, live, last}; after it, {valid bytes nv (0..16)
+    // of the chunk inside the packet's summed region, last}.
+    uint32_t meta[R];
+    uint32_t ilim = 0;  // summed-region end of the job being issued (after the parse)
+    uint32_t lim_mine = HB;
+    auto advance = [&](bool last, bool post) {
+      ic += 8;
+      iaddr += 128;
+      if (__ballot(last) != 0) {  // some group moves to its next job
+        const uint32_t s = gsrc + min(ik + 1, 7u);
+        const uint32_t np = lane_get(jp, s), nnb = lane_get(jnb, s);
+        const uint32_t nlo = lane_get(jlo, s), nhi = lane_get(jhi, s);
+        const uint32_t nlim = post ? lane_get(lim_mine, np) : 0u;
+        if (last) {
+          ++ik;
+          ip = np;
+          inb_ = ik < 8u ? nnb : 0u;
+          ic = gj;
+          iaddr = ((uint64_t)nhi << 32 | nlo) + gj * 16u;
+          ilim = nlim;
+        }
+      }
+    };
+    auto issue_pre = [&](int u) {
+      const bool live = ic < inb_;
+      glds<OO_RX_BODY_AUX>(live ? iaddr : dummy, &L.ring[u][0]);
+      const bool last = inb_ != 0 && ic - gj + 8 >= inb_;
+      meta[u] = ip | (ic << 6) | (live ? M_LIVE : 0u) | (last ? M_LAST : 0u);
+      advance(last, false);
+    };
+    auto issue = [&](int u) {
+      const bool live = ic < inb_;
+      glds<OO_RX_BODY_AUX>(live ? iaddr : dummy, &L.ring[u][0]);
+      const bool last = inb_ != 0 && ic - gj + 8 >= inb_;
+      const int nv = live ? min(max((int)ilim - (HB + 16 * (int)ic), 0), 16) : 0;
+      meta[u] = (uint32_t)nv | (last ? M_LAST : 0u);
+      advance(last, true);
+    };
+
+    // Body prologue (lands during the parse), then wait for the header window.
+#ifdef OO_RX_EXP_LATEPRO
+    if (false) {
+#else
+    if (T >= (uint32_t)R) {
+#endif
+#pragma unroll
+      for (int u = 0; u < R; ++u) issue_pre(u);
+      vm_wait<R>();
+    } else {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if ((uint32_t)u < T) issue_pre(u);
+        else meta[u] = 0;
+      }
+      vm_wait<0>();
+    }
+    STAMP(1, __builtin_amdgcn_s_memrealtime());
+    STAMP(7, T);
+
+    const uint8_t* my = reinterpret_cast<const uint8_t*>(&L.hdr[0][lane]);
     // Header byte j (j >= 0); bytes at or beyond the frame length read 0.
     auto B = [&](int j) -> uint32_t {
       int w = shift + j;
@@ -391,7 +502,17 @@ __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
     auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
     auto N32 = [&](int j) -> uint32_t { return N16(j) | (N16(j + 2) << 16); };
 
-    // ---- 3. parse (per lane)
+#ifdef OO_RX_EXP_STREAMONLY
+    // Experiment build: no parse/demux; every frame's bytes past the window
+    // are summed (timing of the stream machinery alone; records are garbage).
+    oo_gpu_rx_result r;
+    __builtin_memset(&r, 0, sizeof(r));
+    const bool longl4 = span > HB;
+    const int E4 = span;
+    uint32_t s4 = 0, pseudo = 1;
+    const uint32_t proto = 17, flags = 0;
+#else
+    // ---- 4. parse (per lane)
     uint8_t flags = 0;
     int pre_l3 = 14, vlan = 0;
     if (BE16(12) == 0x8100u) {  // ci_parse_rx_vlan (netif_event.c:116-132)
@@ -488,7 +609,7 @@ __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
     if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
 
     // L4 verdict now when the region ends inside the window; otherwise it
-    // waits for the stream (step 5) and the record below is speculative.
+    // waits for the body stream (step 5) and the record below is speculative.
     const bool longl4 = reason == PENDING && need_l4 && E4 > HB;
     if (reason == PENDING && need_l4 && !longl4) {
       uint32_t f = fold16(s4);
@@ -497,7 +618,8 @@ __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
         reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
     }
 
-    // ---- 4. handle_rx_pkt, demux, record (per lane; netif_event.c:250-451).
+    STAMP(2, __builtin_amdgcn_s_memrealtime());
+    // ---- handle_rx_pkt, demux, record (per lane; netif_event.c:250-451).
     oo_gpu_rx_result r;
     r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
     r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
@@ -564,39 +686,64 @@ __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
         const int nst = proto == 6u ? 3 : 2;
         Match m = {-1, 0};
         int stage = 0;
+        // Every stage's first slot bit, its successor's bit and the first
+        // slot's record are loaded up front (two dependent levels); the walks
+        // then usually need nothing more.
         if (is6) {
           const uint32_t zero[4] = {0, 0, 0, 0};
           const uint32_t dx = r.daddr_be, sx = r.saddr_be;
-          const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & P.ip6_mask;
-          const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & P.ip6_mask;
-          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & P.ip6_mask;
-          m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, P.ip6[h1_0]);
+          const uint32_t mask = P.ip6_mask;
+          const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & mask;
+          const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & mask;
+          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
+          const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
+          const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
+          const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
+          const bool o0 = occ_bit(P.occ6, h1_0), o1 = occ_bit(P.occ6, h1_1);
+          const bool o2 = nst == 3 && occ_bit(P.occ6, h1_2);
+          const bool q0 = occ_bit(P.occ6, (h1_0 + h2_0) & mask);
+          const bool q1 = occ_bit(P.occ6, (h1_1 + h2_1) & mask);
+          const bool q2 = nst == 3 && occ_bit(P.occ6, (h1_2 + h2_2) & mask);
+          Slot6 s0 = {}, s1 = {}, s2 = {};
+          if (o0) s0 = load_slot6(P, h1_0);
+          if (o1) s1 = load_slot6(P, h1_1);
+          if (o2) s2 = load_slot6(P, h1_2);
+          m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
           stage = 1;
           if (m.n == 0) {
-            m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, P.ip6[h1_1]);
+            m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
             stage = 2;
           }
           if (m.n == 0 && nst == 3) {
-            m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, P.ip6[h1_2]);
+            m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
             stage = 3;
           }
         } else {
           const uint32_t da = r.daddr_be, sa = r.saddr_be;
-          const uint32_t h1_0 = hash3(da, dport, sa, sport, proto) & P.ip4_mask;
-          const uint32_t h1_1 = hash3(da, dport, 0u, 0u, proto) & P.ip4_mask;
-          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & P.ip4_mask;
-          const uint2 e0 = P.ip4[h1_0];
-          const uint2 e1 = P.ip4[h1_1];
-          uint2 e2 = e1;
-          if (nst == 3) e2 = P.ip4[h1_2];
-          m = walk4(P, da, dport, sa, sport, proto, intf_i, vlan, h1_0, e0);
+          const uint32_t mask = P.ip4_mask;
+          const uint32_t h1_0 = hash3(da, dport, sa, sport, proto) & mask;
+          const uint32_t h1_1 = hash3(da, dport, 0u, 0u, proto) & mask;
+          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
+          const uint32_t h2_0 = hash2(da, dport, sa, sport, proto);
+          const uint32_t h2_1 = hash2(da, dport, 0u, 0u, proto);
+          const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
+          const bool o0 = occ_bit(P.occ4, h1_0), o1 = occ_bit(P.occ4, h1_1);
+          const bool o2 = nst == 3 && occ_bit(P.occ4, h1_2);
+          const bool q0 = occ_bit(P.occ4, (h1_0 + h2_0) & mask);
+          const bool q1 = occ_bit(P.occ4, (h1_1 + h2_1) & mask);
+          const bool q2 = nst == 3 && occ_bit(P.occ4, (h1_2 + h2_2) & mask);
+          Slot4 s0 = {}, s1 = {}, s2 = {};
+          if (o0) s0 = load_slot4(P, h1_0);
+          if (o1) s1 = load_slot4(P, h1_1);
+          if (o2) s2 = load_slot4(P, h1_2);
+          m = walk4(P, da, dport, sa, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
           stage = 1;
           if (m.n == 0) {
-            m = walk4(P, da, dport, 0u, 0u, proto, intf_i, vlan, h1_1, e1);
+            m = walk4(P, da, dport, 0u, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
             stage = 2;
           }
           if (m.n == 0 && nst == 3) {
-            m = walk4(P, 0u, dport, 0u, 0u, proto, intf_i, vlan, h1_2, e2);
+            m = walk4(P, 0u, dport, 0u, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
             stage = 3;
           }
         }
@@ -612,123 +759,85 @@ __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
     }
     r.reason = (uint8_t)reason;
     r.flags = flags;
+#endif
 
-    // ---- 5. stream the tile's long L4 regions as one flat chunk list.
-    const uint32_t nc = longl4 ? (uint32_t)(((E4 + 15) >> 4) - HC) : 0u;
-    const uint32_t incl = wave_scan(nc);
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if (T != 0) {
-      const uint32_t excl = incl - nc;
-      // Chunk f of the flat list (f in [excl, incl) for this packet) is at
-      // VB + 16 f with VB = abase + 16 (HC - excl); window position
-      // 16 (f - excl + HC).
-      const uint64_t vb = abase + (uint64_t)16 * ((uint64_t)HC - (uint64_t)excl);
-      job[lane] = make_uint4((uint32_t)vb, (uint32_t)(vb >> 32), excl, (uint32_t)E4);
 
-      // Buffers of SP pieces of 64 chunks (1 KiB each) into registers, two
-      // buffers in flight: one buffer's loads land while the other is
-      // reduced.  Every load is unconditional (lanes past the list reload
-      // the last chunk, an L2 hit) so the compiler's vmcnt waits are static.
-      //
-      // Chunk -> packet: the packets whose run starts inside the buffer mark
-      // their first chunk in kmap (job lane + 1); a max-scan over the marks,
-      // carried across pieces and buffers (kc), gives every chunk's packet.
-      //
-      // Per-packet sums: G = running sum of the flat list (mod 2^32); the
-      // chunk that starts a packet's run records G before it, the one that
-      // ends it records G after it, so sum = g_end - g_start.  Plain LDS
-      // writes, nothing to wait for inside the stream.
-      uint32_t kc = 1;  // mark (job lane + 1) of the packet running into the next buffer
-      uint32_t G = 0;   // running sum of the flat list before the buffer being reduced
-      // meta per piece: job lane (7 bits) | chunk index in the run (10) | run end E4 (14);
-      // all ones = past the list.
-      auto issue = [&](uint4 (&buf)[SP], uint32_t F0, uint32_t (&meta)[SP]) {
-        const uint32_t ln = opaque((uint32_t)lane);
-        const uint32_t ex = opaque(excl);
+
+    // ---- 5. body stream.  Each lane sums its chunk, masked at the L4 region
+    // end (lim of its packet); on a group's last round of a packet the 8-lane
+    // total goes to lane (g, job number), whose packet lane collects it
+    // below.  Packets whose verdict is already final sum nothing (lim = HB).
+#ifdef OO_RX_EXP_LATEPRO
 #pragma unroll
-        for (int w = 0; w < SP / 4; ++w) reinterpret_cast<uint32_t*>(kmap)[w * 64 + ln] = 0;
-        if (nc != 0 && ex >= F0 && ex < F0 + SP * 64) kmap[ex - F0] = (uint8_t)(ln + 1);
-        wave_sync_lds();
-        uint32_t m[SP];
+    for (int u = 0; u < R; ++u) {
+      if ((uint32_t)u < T) issue_pre(u);
+      else meta[u] = 0;
+    }
+#endif
+    lim_mine = longl4 ? (uint32_t)E4 : (uint32_t)HB;
+    ilim = lane_get(lim_mine, ip);
 #pragma unroll
-        for (int u = 0; u < SP; ++u) m[u] = kmap[u * 64 + ln];
-#pragma unroll
-        for (int u = 0; u < SP; ++u) {
-          m[u] = max(wave_max_scan(m[u]), kc);
-          kc = (uint32_t)__builtin_amdgcn_readlane((int)m[u], 63);
+    for (int u = 0; u < R; ++u) {  // the prologue's meta, now that lim is known
+      const uint32_t mt = meta[u];
+      const int lim = (int)lane_get(lim_mine, mt & 63u);
+      const int nv = min(max(lim - (HB + 16 * (int)((mt >> 6) & 1023u)), 0), 16);
+      meta[u] = (mt & M_LIVE ? (uint32_t)nv : 0u) | (mt & M_LAST);
+    }
+    uint32_t acc = 0, bs = 0, ck = 0;
+    auto consume = [&](int u) {
+      const uint32_t mt = meta[u];
+      const uint4 v = lds_read16(&L.ring[u][lane]);
+      const int nv = (int)(mt & 31u);
+      if (nv == 16) acc = chunk_sum_all(v, acc);
+      else if (nv != 0) acc += chunk_sum(v, 0, 0, nv);
+      if (__ballot((mt & M_LAST) != 0) != 0) {
+        const uint32_t t = group_sum8(acc);
+        if (mt & M_LAST) {
+          if (gj == ck) bs = t;
+          ++ck;
+          acc = 0;
         }
-        uint4 jk[SP];
-#pragma unroll
-        for (int u = 0; u < SP; ++u) jk[u] = job[m[u] - 1];
-#pragma unroll
-        for (int u = 0; u < SP; ++u) {
-          const uint32_t f = F0 + ln + (uint32_t)(u * 64);
-          const uint32_t fc = f < T ? f : T - 1;
-          const uint64_t src = (((uint64_t)jk[u].y << 32) | jk[u].x) + (uint64_t)16 * fc;
-          buf[u] = ld_stream(src);
-          meta[u] = f < T ? (m[u] - 1) | ((f - jk[u].z) << 7) | (jk[u].w << 17) : 0xffffffffu;
-        }
-      };
-      auto consume = [&](const uint4 (&buf)[SP], const uint32_t (&meta)[SP]) {
-#pragma unroll
-        for (int u = 0; u < SP; ++u) {
-          const uint32_t mt = meta[u];
-          const bool live = mt != 0xffffffffu;
-          const uint32_t kf = mt & 127u;
-          const int p = (int)(((mt >> 7) & 1023u) + HC) * 16;
-          const int e4 = (int)(mt >> 17);
-          uint32_t val = 0;
-          if (live) val = p + 16 <= e4 ? chunk_sum_all(buf[u], 0u) : chunk_sum(buf[u], p, 0, e4);
-          const uint32_t sc = wave_scan(val);
-          const uint32_t g = G + sc;
-          if (live && p == HC * 16) g_start[kf] = g - val;
-          if (live && p + 16 >= e4) g_end[kf] = g;
-          G += (uint32_t)__builtin_amdgcn_readlane((int)sc, 63);
-        }
-      };
-      uint4 ba[SP], bb[SP];
-      uint32_t ma[SP], mb[SP];
-      constexpr uint32_t R = SP * 64;  // chunks per buffer
-      issue(ba, 0, ma);
-      issue(bb, R, mb);
-      for (uint32_t F = 0; F < T; F += 2 * R) {
-        // sched_barrier: keep each buffer's reloads after its reduction, so
-        // only two buffers are ever live.
-        consume(ba, ma);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(ba, F + 2 * R, ma);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(bb, mb);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(bb, F + 3 * R, mb);
-        __builtin_amdgcn_sched_barrier(0);
       }
-      wave_sync_lds();
-      const uint32_t jacc = longl4 ? g_end[lane] - g_start[lane] : 0u;
-      s4 += jacc;
-      if (longl4) {
-        // The verdict the speculative record waited for; a failure turns it
-        // into the drop record (only the fields a drop defines survive).
-        uint32_t f = fold16(s4);
-        if (shift & 1) f = swap16(f);
-        if (fold16(f + pseudo) != 0xffffu) {
-          r.reason = (uint8_t)(proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM);
-          r.flags = (uint8_t)(flags & (OO_RX_F_VLAN | OO_RX_F_IP6));
-          r.stage = 0; r.l4_off = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
-          r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+    };
+    STAMP(3, __builtin_amdgcn_s_memrealtime());
+    for (uint32_t k0 = 0; k0 < T; k0 += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const uint32_t k = k0 + (uint32_t)u;
+        if (k < T) {
+          // Pieces k+1 .. min(T, k+R)-1 may still be in flight.
+          if (k + R <= T) vm_wait<R - 1>();
+          else vm_wait<0>();
+          consume(u);
+          if (k + R < T) issue(u);  // slot u was read (lds_read16 waited)
         }
       }
     }
+    const uint32_t body = lane_get(bs, myslot);
+    STAMP(4, __builtin_amdgcn_s_memrealtime());
 
+    if (longl4) {
+      // The verdict the speculative record waited for; a failure turns it
+      // into the drop record (only the fields a drop defines survive).
+      s4 += body;
+      uint32_t f = fold16(s4);
+      if (shift & 1) f = swap16(f);
+      if (fold16(f + pseudo) != 0xffffu) {
+        r.reason = (uint8_t)(proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM);
+        r.flags = (uint8_t)(flags & (OO_RX_F_VLAN | OO_RX_F_IP6));
+        r.stage = 0; r.l4_off = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
+        r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+      }
+    }
 
     if (valid) {
+      atomicAdd(&ctr[r.reason & (OO_RX_R_COUNT - 1)], 1u);
       uint4* o = reinterpret_cast<uint4*>(P.out + idx);
       const uint4* src = reinterpret_cast<const uint4*>(&r);
       o[0] = src[0];
       o[1] = src[1];
-      atomicAdd(&ctr[r.reason & (OO_RX_R_COUNT - 1)], 1u);
     }
-    wave_sync_lds();  // LDS is restaged by the next tile
+    STAMP(5, __builtin_amdgcn_s_memrealtime());
   }
 
   __syncthreads();

@@ -1,0 +1,184 @@
+// SPDX-License-Identifier: BSD-2-Clause
+// Streaming-ring probe: how much LDS-DMA must a CU keep in flight to read
+// HBM near its ceiling when every wave streams through a continuous ring of
+// R 1-KiB slots with a counted `s_waitcnt vmcnt(R-1)` (never a full drain)?
+// Each wave owns a contiguous span of the buffer.  Prints one JSON line per
+// (slots per wave, waves per block, blocks per CU).
+// Build: make tools/ring_probe
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t dot(uint32_t w, uint32_t acc) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(v2u16, w),
+                                __builtin_bit_cast(v2u16, 0x00010001u), acc, false);
+}
+
+template <int R, int W>
+__global__ __launch_bounds__(64 * W) void ring(const u32x4* __restrict__ p, size_t npieces,
+                                               uint32_t* out) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  u32x4* slot0 = lds + (size_t)w * R * 64;
+  const size_t waves = (size_t)gridDim.x * W;
+  const size_t gw = (size_t)blockIdx.x * W + w;
+  const size_t per = (npieces + waves - 1) / waves;
+  const size_t b = gw * per;
+  const size_t e = b + per < npieces ? b + per : npieces;
+  uint32_t acc = 0;
+  if (b < e) {
+    const size_t last = e - 1;
+    // prologue: R pieces in flight (pieces past the span reload the last one)
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const size_t pc = b + u <= last ? b + u : last;
+      __builtin_amdgcn_global_load_lds((const void*)(p + pc * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(slot0 + u * 64),
+                                       16, 0, 2);
+    }
+    for (size_t i = b; i < e; i += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        wait_vm<R - 1>();
+        const u32x4 v = slot0[u * 64 + lane];
+        acc = dot(v.x, dot(v.y, dot(v.z, dot(v.w, acc))));
+        const size_t nx = i + R + u;
+        const size_t pc = nx <= last ? nx : last;
+        __builtin_amdgcn_global_load_lds((const void*)(p + pc * 64 + lane),
+                                         (void __attribute__((address_space(3)))*)(slot0 + u * 64),
+                                         16, 0, 2);
+      }
+    }
+    wait_vm<0>();
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int R, int W>
+static void run(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
+  const size_t lds = (size_t)R * W * 1024;
+  int bpc = 0;
+  (void)hipFuncSetAttribute((const void*)ring<R, W>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, ring<R, W>, 64 * W, lds);
+  for (int m : {1, 2, 3, 4, 5, 6, 8, 10, 12, 16}) {
+    if (m > bpc) break;
+    const int grid = cu * m;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    float best = 1e9f;
+    for (int r = 0; r < 10; ++r) {
+      (void)hipEventRecord(e0, 0);
+      hipLaunchKernelGGL((ring<R, W>), dim3(grid), dim3(64 * W), lds, 0, a, bytes / 1024, o);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (r >= 2 && ms < best) best = ms;
+    }
+    printf("{\"slots\":%d,\"waves_per_block\":%d,\"blocks_per_cu\":%d,\"kib_in_flight_per_cu\":%d,"
+           "\"GBps\":%.1f}\n",
+           R, W, m, R * W * m, bytes / (best * 1e-3) / 1e9);
+  }
+}
+
+
+// Grouped variant: each wave owns 64-frame tiles of FB-byte frames; groups
+// of G lanes stream one frame each (G*16 contiguous bytes per round), so an
+// instruction touches 64/G frames.
+template <int R, int G>
+__global__ __launch_bounds__(64) void ring_grp(const u32x4* __restrict__ p, size_t nframes,
+                                               uint32_t* out) {
+  constexpr uint32_t fb16 = 96;
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  const int lane = threadIdx.x;
+  const int g = lane / G, j = lane % G;
+  constexpr int NG = 64 / G;
+  const size_t ntiles = nframes / 64;
+  constexpr uint32_t rounds = (fb16 + G - 1) / G;  // rounds per frame per group
+  uint32_t acc = 0;
+  for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // group g streams frames t*64 + g, + NG, ...: (64/NG) frames x rounds
+    const uint32_t total = (64 / NG) * rounds;
+    auto src = [&](uint32_t k) {
+      const uint32_t fi = k / rounds, r = k % rounds;
+      const uint32_t c = r * G + j;
+      const size_t frame = t * 64 + g + fi * NG;
+      return (k < total && c < fb16) ? p + frame * fb16 + c : p;
+    };
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      __builtin_amdgcn_global_load_lds((const void*)src(u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
+    for (uint32_t k0 = 0; k0 < total; k0 += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        wait_vm<R - 1>();
+        const u32x4 v = lds[u * 64 + lane];
+        acc = dot(v.x, dot(v.y, dot(v.z, dot(v.w, acc))));
+        __builtin_amdgcn_global_load_lds((const void*)src(k0 + R + u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
+      }
+    }
+    wait_vm<0>();
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int R, int G>
+static void run_grp(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
+  const size_t lds = (size_t)R * 1024;
+  const size_t nframes = bytes / 1536 / 64 * 64;
+  int bpc = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, ring_grp<R, G>, 64, lds);
+  for (int m : {4, 8, 12, 16}) {
+    if (m > bpc) break;
+    const int grid = cu * m;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    float best = 1e9f;
+    for (int r = 0; r < 10; ++r) {
+      (void)hipEventRecord(e0, 0);
+      hipLaunchKernelGGL((ring_grp<R, G>), dim3(grid), dim3(64), lds, 0, a, nframes, o);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (r >= 2 && ms < best) best = ms;
+    }
+    if (hipGetLastError() != hipSuccess) { printf("launch error\n"); exit(1); }
+    printf("{\"grouped\":%d,\"slots\":%d,\"waves_per_cu\":%d,\"GBps\":%.1f}\n", G, R, m,
+           nframes * 1536 / (best * 1e-3) / 1e9);
+  }
+}
+
+int main(int argc, char** argv) {
+  const size_t bytes = (argc > 1 ? strtoull(argv[1], 0, 0) : (size_t)1610612736);
+  u32x4* a;
+  uint32_t* o;
+  if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&o, 4) != hipSuccess) return 1;
+  (void)hipMemset(a, 1, bytes);
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, 0);
+  const int cu = prop.multiProcessorCount;
+  if (argc > 2) {
+    run<8, 1>(a, bytes, o, cu);
+    run<16, 1>(a, bytes, o, cu);
+    run<32, 1>(a, bytes, o, cu);
+  }
+  run_grp<4, 8>(a, bytes, o, cu);
+  run_grp<6, 8>(a, bytes, o, cu);
+  run_grp<4, 16>(a, bytes, o, cu);
+  run_grp<4, 32>(a, bytes, o, cu);
+  run_grp<4, 64>(a, bytes, o, cu);
+  run_grp<8, 64>(a, bytes, o, cu);
+  return 0;
+}

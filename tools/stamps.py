@@ -1,0 +1,100 @@
+# SPDX-License-Identifier: BSD-2-Clause
+"""Per-wave phase timeline of one rx_kernel launch (diagnostic).
+
+Needs a library built with -DOO_RX_STAMPS (``make variants
+VARIANTS="st:-DOO_RX_STAMPS"``), selected with OO_RX_LIB.  Prints where a
+wave's time goes per tile (header wait, parse, body stream, record) and how
+the waves' finish times spread.
+
+    OO_RX_LIB=build/var_st.so python tools/stamps.py --config 2
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--n", type=int, default=0)
+    args = ap.parse_args()
+    import torch
+
+    from bench import DEFAULT_N
+    from onload_amd import pktgen
+    from onload_amd.rx import GpuRxStack
+
+    dev = torch.device("cuda", 0)
+    n = args.n or DEFAULT_N[args.config]
+    filters, socks = pktgen.world(args.config)
+    buf, desc = pktgen.generate(args.config, n)
+    g = GpuRxStack(device=0)
+    g.load_world(filters, socks)
+    lib = g._lib
+    lib.oo_gpu_rx_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.oo_gpu_rx_debug_grid.argtypes = [ctypes.c_void_p]
+    grid = lib.oo_gpu_rx_debug_grid(g._ctx)
+    frames = torch.from_numpy(buf).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    waves = grid * 4  # upper bound on waves per block
+    st = torch.zeros(waves * 64 * 8, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    g.sync(s)
+    for _ in range(3):
+        g.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
+                              out.data_ptr(), 0, s)
+    lib.oo_gpu_rx_debug_stamps(g._ctx, ctypes.c_void_p(st.data_ptr()))
+    torch.cuda.synchronize(dev)
+    g.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
+                          out.data_ptr(), 0, s)
+    torch.cuda.synchronize(dev)
+    a = st.cpu().numpy().reshape(waves, 64, 8)
+    used = a[:, :, 0] != 0
+    t0 = a[:, :, 0][used].min()
+    ns = 10.0  # s_memrealtime is 100 MHz
+    rows = []
+    for w in range(waves):
+        k = int(used[w].sum())
+        if k == 0:
+            continue
+        rows.append((w, k, (a[w, k - 1, 5] - t0) * ns, (a[w, 0, 0] - t0) * ns))
+    rows = np.array(rows)
+    ph = a[used]
+    d = lambda i, j: (ph[:, j] - ph[:, i]) * ns  # noqa: E731
+    res = {
+        "waves": int(len(rows)), "grid_blocks": grid,
+        "tiles_per_wave": {str(int(k)): int((rows[:, 1] == k).sum()) for k in np.unique(rows[:, 1])},
+        "kernel_span_us": float(rows[:, 2].max() / 1e3),
+        "wave_end_us_pct": [float(np.percentile(rows[:, 2], q) / 1e3) for q in (0, 10, 50, 90, 100)],
+        "wave_start_us_max": float(rows[:, 3].max() / 1e3),
+        "per_tile_us_mean": {
+            "hdr_wait": float(d(0, 1).mean() / 1e3), "parse": float(d(1, 2).mean() / 1e3),
+            "demux": float(d(2, 3).mean() / 1e3), "stream": float(d(3, 4).mean() / 1e3),
+            "record": float(d(4, 5).mean() / 1e3), "total": float(d(0, 5).mean() / 1e3),
+            "gap_to_next": float(np.mean([(a[w, i + 1, 0] - a[w, i, 5]) * ns
+                                          for w in range(waves) for i in range(int(used[w].sum()) - 1)]) / 1e3),
+        },
+        "rounds_mean": float(ph[:, 7].mean()),
+        "stream_ns_per_round": float((d(3, 4) / np.maximum(ph[:, 7], 1)).mean()),
+    }
+    # per-XCD view: blocks are dealt round-robin to the 8 XCDs
+    wpb = max(1, waves // grid)
+    ends = {}
+    for w, k, e, _ in rows:
+        ends.setdefault(int(w) // 4 % 8, []).append(e / 1e3)
+    res["end_us_by_xcd(block%8)"] = {x: round(float(np.mean(v)), 1) for x, v in sorted(ends.items())}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
