@@ -27,9 +27,9 @@
 
 #include "oo_rx_device.h"
 
-extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
-extern "C" int oo_rx_blocks_per_cu(void);
-extern "C" int oo_rx_waves_per_block(void);
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int split, int grid, hipStream_t stream);
+extern "C" int oo_rx_blocks_per_cu(int split);
+extern "C" int oo_rx_waves_per_block(int split);
 
 namespace {
 
@@ -121,7 +121,10 @@ struct oo_gpu_rx_ctx {
   uint32_t* d_occ4 = nullptr;
   Slot6* d_slot6 = nullptr;
   uint32_t* d_occ6 = nullptr;
-  uint32_t grid = 1024;  // resident blocks of the persistent kernel
+  uint32_t grid = 1024;        // resident blocks of rx_kernel
+  uint32_t grid_split = 1024;  // resident blocks of rx_split
+  uint32_t split_min = 512;    // mean bytes per frame from which rx_split runs
+  int kernel_force = -1;       // OO_RX_KERNEL: 0 = rx_kernel, 1 = rx_split
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
   // host-path staging
   uint64_t stage_bytes = 0;
@@ -441,14 +444,20 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
     return 0;
   }
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
-  {
-    // Persistent grid: every resident block (occupancy query), optionally
+  if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) {
+    // Persistent grids: every resident block (occupancy query), optionally
     // scaled by OO_RX_GRID_PCT for tuning.
-    const int bpc = oo_rx_blocks_per_cu();
-    if (bpc > 0)
-      c->grid = std::max<uint32_t>(1, (uint32_t)(bpc * prop.multiProcessorCount) *
-                                          env_u32("OO_RX_GRID_PCT", 100) / 100);
+    const uint32_t pct = env_u32("OO_RX_GRID_PCT", 100);
+    const int b0 = oo_rx_blocks_per_cu(0), b1 = oo_rx_blocks_per_cu(1);
+    if (b0 > 0)
+      c->grid = std::max<uint32_t>(1, (uint32_t)(b0 * prop.multiProcessorCount) * pct / 100);
+    if (b1 > 0)
+      c->grid_split = std::max<uint32_t>(1, (uint32_t)(b1 * prop.multiProcessorCount) * pct / 100);
+  }
+  c->split_min = env_u32("OO_RX_SPLIT_MIN", c->split_min);
+  if (const char* k = getenv("OO_RX_KERNEL")) {
+    if (!strcmp(k, "split")) c->kernel_force = 1;
+    if (!strcmp(k, "lanes")) c->kernel_force = 0;
   }
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->d_slot4, sizeof(Slot4) * c->slot4.size()) == hipSuccess &&
@@ -576,19 +585,23 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.occ6 = c->d_occ6;
   P.stamps = c->stamps;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
-  // Static balanced partition: W resident waves each take k tiles of
-  // P.tile <= 64 packets, k = ceil(n / (64 W)), P.tile = ceil(n / (W k)), so
-  // no wave does more than one tile's worth of packets beyond the average
-  // (a 64-packet tiling of 2^20 packets over 2560 waves would leave 40% of
-  // the waves running a 7th tile alone).  Small batches use fewer blocks.
-  const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
+  // rx_split (parser + streamer waves) for large frames, rx_kernel otherwise;
+  // the frame buffer's bytes per descriptor estimate the mean frame size.
+  const int split = c->kernel_force >= 0 ? c->kernel_force
+                                         : (frames_bytes >= (uint64_t)c->split_min * n ? 1 : 0);
+  // Static balanced partition: the W tile-processing waves (rx_split's
+  // streamers) each take k tiles of P.tile <= 64 packets,
+  // k = ceil(n / (64 W)), P.tile = ceil(n / (W k)).  Small batches use
+  // fewer blocks.
+  const uint32_t wpb = (uint32_t)oo_rx_waves_per_block(split);
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
+  const uint32_t cap = split ? c->grid_split : c->grid;
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, cap));
   const uint64_t W = (uint64_t)blocks * wpb;
   const uint64_t k = (n + 64 * W - 1) / (64 * W);
   P.tile = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (n + W * k - 1) / (W * k)));
   const int grid = (int)blocks;
-  return oo_rx_launch(&P, grid, s) == 0 ? 0 : -EIO;
+  return oo_rx_launch(&P, split, grid, s) == 0 ? 0 : -EIO;
 }
 
 int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,

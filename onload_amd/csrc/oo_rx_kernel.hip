@@ -1,6 +1,6 @@
 // SPDX-License-Identifier: BSD-2-Clause
 //
-// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernel for Onload's software
+// oo_rx_kernel.hip -- gfx950 (MI355X / CDNA4) kernels for Onload's software
 // receive transform: checksum verify + header parse + 4-tuple socket demux.
 //
 // Reference semantics (file:line in /root/reference):
@@ -17,29 +17,33 @@
 //   ci_netif_filter_for_each_match[_ip6]  netif_table.c:234-319, netif_table_ip6.c:110-189
 //   __onload_hash1/2/3            src/include/onload/hash.h:84-173
 //
-// One persistent kernel, rx_kernel (DESIGN.md "Kernel").  Each wave owns
-// tiles of 64 packets (one packet per lane for parse/demux) and strides over
-// them.  Every HBM read of frame bytes and descriptors is an LDS-DMA
-// (global_load_lds_dwordx4, nontemporal) whose completion the wave counts
-// itself with `s_waitcnt vmcnt(N)`; only the filter-table probes are plain
-// loads.  Per tile:
-//   1. descriptors: one 1-KiB LDS-DMA piece (the next tile's is issued as
-//      soon as this one is read);
-//   2. header window: the first 128 bytes of each frame, 8 pieces, lane =
-//      packet, landing transposed as [chunk][packet] 16-B cells;
-//   3. body: the frame bytes past the window, streamed through a ring of R
-//      1-KiB slots.  Eight lanes (an 8-lane group, 128 contiguous bytes per
-//      round) stream one packet at a time; the tile's packets with a body are
-//      dealt round-robin to the wave's eight groups.  The first R pieces are
-//      issued before the parse, so they land while it runs;
-//   4. per lane: VLAN, L3/L4 gates, pseudo-header, window sums, handle_rx_pkt's
-//      frag/options/TCP-scattered tests, the 2 or 3 lookup stages, a
-//      speculative 32-B record;
-//   5. the body stream: every lane sums its 16-B chunk (masked at the L4
-//      region end), accumulates per packet, and an 8-lane DPP reduction hands
-//      each packet's body sum to its parse lane, which then decides the
-//      verdict the record waited for.
-//   Per-reason counters accumulate in LDS and are flushed once per block.
+// Work unit: a tile of up to 64 packets.  Per packet the transform splits
+// into
+//   * the header work: the first 128 bytes of the frame (the "window") are
+//     parsed one packet per lane -- VLAN, L3/L4 gates, pseudo-header, IPv4
+//     header sum, the L4 sum inside the window, handle_rx_pkt's
+//     frag/options/TCP-scattered tests and the 2 or 3 lookup stages --
+//     giving a 32-B record that is final unless the L4 region runs past the
+//     window (parse_packet);
+//   * the body: the frame bytes past the window, summed by 8-lane groups
+//     (128 contiguous bytes per group per round, one packet per group at a
+//     time) from a ring of 1-KiB LDS-DMA pieces (Body).  Only the
+//     descriptors decide the body, so it can be in flight before the parse.
+// The verdict of a long packet adds the body sum to the window part.
+//
+// Two kernels (DESIGN.md "Kernels"):
+//   rx_split  -- large frames.  A block is one parser wave and WS streamer
+//                waves.  Streamers only stream bodies, through a ring that
+//                never drains between tiles; the parser parses the tiles the
+//                streamers are streaming and finalises the previous ones.
+//                One barrier per tile phase.
+//   rx_kernel -- any traffic (the small-frame path).  Every wave parses and
+//                streams its own tiles.
+// Every frame-byte and descriptor read in the streaming code is an LDS-DMA
+// (global_load_lds_dwordx4) whose completion the wave counts itself with
+// s_waitcnt vmcnt(N); the LDS reads that follow are inline asm, because
+// hipcc waits vmcnt(0) before any LDS access it sees while LDS-DMA is in
+// flight.
 //
 // The verdict uses the mod-0xffff residue of the exact word sum; see
 // oracle/rx_oracle.c for why that equals the reference's folded-complement
@@ -58,22 +62,26 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Tuning knobs (compile-time; `make variants` builds sweeps of them).
 #ifndef OO_RX_WAVES
-#define OO_RX_WAVES 2
+#define OO_RX_WAVES 2  // rx_kernel: waves per block
 #endif
 #ifndef OO_RX_RING
-#define OO_RX_RING 6
+#define OO_RX_RING 6  // rx_kernel: body ring slots per wave (even)
 #endif
-#ifndef OO_RX_WPE
-#define OO_RX_WPE 0  // amdgpu_waves_per_eu target, 0 = compiler's choice
+#ifndef OO_RX_WS
+#define OO_RX_WS 2  // rx_split: streamer waves per block (plus one parser)
+#endif
+#ifndef OO_RX_SRING
+#define OO_RX_SRING 8  // rx_split: body ring slots per streamer
 #endif
 
-constexpr int WAVES = OO_RX_WAVES;   // waves per block
-constexpr int R = OO_RX_RING;        // body ring slots (1 KiB each) per wave
+constexpr int WAVES = OO_RX_WAVES;
+constexpr int R = OO_RX_RING;
+static_assert(R % 2 == 0, "rx_kernel consumes its ring two pieces at a time");
+constexpr int WS = OO_RX_WS;
+constexpr int SR = OO_RX_SRING;
 constexpr int HC = 8;                // staged header chunks per packet
 constexpr int HB = HC * 16;          // staged window bytes per packet
-constexpr int ROWB = 64 * 16;        // one staged chunk of all 64 packets
-constexpr uint32_t M_LIVE = 1u << 16;  // body meta: chunk inside the frame
-constexpr uint32_t M_LAST = 1u << 17;  // body meta: the group's last round of the packet
+constexpr int ROWB = 64 * 16;        // one staged chunk of all 64 packets (LDS-DMA rows)
 
 // Filter-table entry states (netif_table.c:34-42).
 constexpr uint32_t ST_MASK = 0xc0000000u;
@@ -122,6 +130,15 @@ __device__ __forceinline__ uint4 lds_read16(const void* p) {
   return v;
 }
 
+// Two 16-B LDS reads, one wait (early-clobber outputs: the second read must
+// not take its address from a register the first is already writing).
+__device__ __forceinline__ void lds_read16x2(const void* p0, const void* p1, uint4& v0, uint4& v1) {
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(v0), "=&v"(v1)
+               : "v"((uint32_t)(uintptr_t)(lptr)(p0)), "v"((uint32_t)(uintptr_t)(lptr)(p1))
+               : "memory");
+}
+
 // Value of v in lane src (ds_bpermute: no LDS memory access, so it needs no
 // vmcnt wait).  Call with every lane active.
 __device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
@@ -132,11 +149,6 @@ __device__ __forceinline__ bool occupied(uint32_t st) {
   return ((~st) & ST_EMPTY & ST_TOMBSTONE) != 0;
 }
 
-__device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // hash.h:84-93 / 165-173; network-order values in host integers.
 __device__ __forceinline__ uint32_t hash3(uint32_t la, uint32_t lp, uint32_t ra,
@@ -325,53 +337,534 @@ __device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp, cons
 }
 
 
+
+// ---------------------------------------------------------------------------
+// Header work of one packet (one lane).
+
+// What the parse leaves for the verdict.
+struct Parsed {
+  oo_gpu_rx_result r;  // the record; final unless the verdict waits for the body
+  uint32_t s4;         // window-word sum of the L4 region's bytes in the window,
+                       // minus its complement past the window (mod 2^32)
+  uint32_t pseudo;     // pseudo-header word sum
+  uint32_t odd_long;   // bit 0: odd frame address (RFC 1071 byte swap);
+                       // bit 1: the L4 region runs past the window
+};
+
+// Window-word sum of window bytes [S, E) read from HBM (the rare L4 region
+// that ends before the frame does, past the window).
+__device__ __noinline__ uint32_t window_sum_global(uint64_t abase, int S, int E) {
+  uint32_t s = 0;
+  for (int c = S >> 4; c * 16 < E; ++c) {
+    const uint4 v = *reinterpret_cast<const uint4*>(abase + (uint64_t)c * 16);
+    s += chunk_sum(v, c * 16, S, E);
+  }
+  return s;
+}
+
+// handle_rx_csum_bad + handle_rx_pkt + the lookup stages for the packet whose
+// window starts at `my` (16-B cells, rows RB bytes apart; window byte w of
+// the frame's 16-B-aligned start is my[(w >> 4) * RB + (w & 15)]).
+template <int RB>
+__device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* my, int shift,
+                                               int len, int intf_i, uint64_t abase, int span) {
+  // Header byte j (j >= 0); bytes at or beyond the frame length read 0.
+  auto B = [&](int j) -> uint32_t {
+    int w = shift + j;
+    w = w < HB ? w : HB - 1;
+    const uint32_t v = my[(w >> 4) * RB + (w & 15)];
+    return j < len ? v : 0u;
+  };
+  auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
+  auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
+  auto N32 = [&](int j) -> uint32_t { return N16(j) | (N16(j + 2) << 16); };
+
+  uint8_t flags = 0;
+  int pre_l3 = 14, vlan = 0;
+  if (BE16(12) == 0x8100u) {  // ci_parse_rx_vlan (netif_event.c:116-132)
+    pre_l3 = 18;
+    vlan = (int)(BE16(14) & 0xfffu);
+    flags |= OO_RX_F_VLAN;
+  }
+  const int l3 = pre_l3;
+  uint32_t reason = PENDING;
+  bool is6 = false, l3ok = false;
+  int ip_len = 0, ihl4 = 0, ip_paylen = 0, l4 = 0;
+  uint32_t proto = 0;
+  if (len < pre_l3 + 20) {  // netif_event.c:1030
+    reason = OO_RX_R_SHORT_L2;
+  } else {
+    const uint32_t et = BE16(pre_l3 - 2);
+    if (et == 0x0800u) {  // :1038-1058
+      l3ok = true;
+      ip_len = (int)BE16(l3 + 2);
+      ihl4 = (int)(B(l3) & 0xfu) * 4;
+      ip_paylen = ip_len - ihl4;
+      proto = B(l3 + 9);
+      if (ip_paylen <= 0 || len < pre_l3 + ip_len) reason = OO_RX_R_IP4_LEN;
+      l4 = l3 + ihl4;
+    } else if (et == 0x86ddu) {  // :1060-1076
+      l3ok = true;
+      is6 = true;
+      flags |= OO_RX_F_IP6;
+      ip_paylen = (int)BE16(l3 + 4);
+      proto = B(l3 + 6);
+      if (ip_paylen <= 0 || len < pre_l3 + 40 + ip_paylen) reason = OO_RX_R_IP6_LEN;
+      l4 = l3 + 40;
+    } else {
+      reason = OO_RX_R_NOT_IP;  // :1078
+    }
+  }
+
+  // L4 gates (netif_event.c:1084-1127) -> which region to sum.
+  uint32_t l4_gate = PENDING;
+  bool need_l4 = false;
+  int l4_len = 0;
+  uint32_t pseudo = 0;
+  if (reason == PENDING) {
+    if (proto == 6u) {
+      const int hlen = (int)((B(l4 + 12) & 0xf0u) >> 2);
+      if (ip_paylen < 20) l4_gate = OO_RX_R_TCP_SHORT;
+      else if (hlen < 20 || ip_paylen < hlen) l4_gate = OO_RX_R_TCP_CSUM;
+      else { need_l4 = true; l4_len = ip_paylen; }
+    } else if (proto == 17u) {
+      const uint32_t udp_len = BE16(l4 + 4);
+      if (ip_paylen < 8) l4_gate = OO_RX_R_UDP_SHORT;
+      else if (udp_len < 8u || udp_len > (uint32_t)ip_paylen) l4_gate = OO_RX_R_UDP_CSUM;
+      else if (!(N16(l4 + 6) == 0u && !is6)) { need_l4 = true; l4_len = (int)udp_len; }
+    } else {
+      l4_gate = OO_RX_R_PROTO_OTHER;
+    }
+    if (need_l4) {
+      // Pseudo-header words (checksum.c:215-223, 304-305, 334-335).
+      if (is6) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a += N16(l3 + 8 + 2 * i);
+        pseudo = a + (proto == 6u ? N16(l3 + 4) + 0x0600u : N16(l4 + 4) + 0x1100u);
+      } else {
+        pseudo = N16(l3 + 12) + N16(l3 + 14) + N16(l3 + 16) + N16(l3 + 18);
+        if (proto == 6u) {
+          const uint32_t pl = (uint32_t)ip_paylen & 0xffffu;
+          pseudo += 0x0600u + (((pl & 0xffu) << 8) | (pl >> 8));
+        } else {
+          pseudo += 0x1100u + N16(l4 + 4);
+        }
+      }
+    }
+  }
+
+  // Sums over the staged window: IPv4 header [S3,E3), L4 head [S4,min(E4,HB)).
+  const bool need_ip = reason == PENDING && !is6;
+  const int S3 = shift + l3, E3 = need_ip ? shift + l3 + ihl4 : S3;
+  const int S4 = shift + l4, E4 = need_l4 ? shift + l4 + l4_len : S4;
+  const int E4h = E4 < HB ? E4 : HB;
+  uint32_t s3 = 0, s4 = 0;
+  if (need_ip || need_l4) {
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(my + k * RB);
+      if (k * 16 < E3) s3 += chunk_sum(v, k * 16, S3, E3);
+      if (k * 16 < E4h) s4 += chunk_sum(v, k * 16, S4, E4h);
+    }
+  }
+  if (reason == PENDING && need_ip) {
+    // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
+    if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
+  }
+  if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
+
+  // L4 verdict now when the region ends inside the window; otherwise it
+  // waits for the body stream (step 5) and the record below is speculative.
+  const bool longl4 = reason == PENDING && need_l4 && E4 > HB;
+  if (reason == PENDING && need_l4 && !longl4) {
+    uint32_t f = fold16(s4);
+    if (shift & 1) f = swap16(f);  // RFC 1071 byte-order swap
+    if (fold16(f + pseudo) != 0xffffu)
+      reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+  }
+
+  // ---- handle_rx_pkt, demux, record (per lane; netif_event.c:250-451).
+  oo_gpu_rx_result r;
+  r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
+  r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
+  r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+  if (l3ok) {
+    r.proto = (uint8_t)proto;
+    r.ip_paylen = (uint16_t)ip_paylen;
+  }
+  if (reason == PENDING) {
+    flags |= OO_RX_F_CSUM_OK;
+    r.l4_off = (uint16_t)l4;
+    const uint32_t sport = N16(l4), dport = N16(l4 + 2);
+    r.sport_be = (uint16_t)sport;
+    r.dport_be = (uint16_t)dport;
+    uint32_t a6s[4], a6d[4];
+    if (is6) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a6s[i] = N32(l3 + 8 + 4 * i);
+        a6d[i] = N32(l3 + 24 + 4 * i);
+      }
+      r.saddr_be = a6s[0] ^ a6s[1] ^ a6s[2] ^ a6s[3];
+      r.daddr_be = a6d[0] ^ a6d[1] ^ a6d[2] ^ a6d[3];
+    } else {
+      r.saddr_be = N32(l3 + 12);
+      r.daddr_be = N32(l3 + 16);
+      const uint32_t frag = BE16(l3 + 6);
+      if ((frag & 0x3fffu) != 0 || ip_len > len - pre_l3) {
+        reason = OO_RX_R_IP4_FRAG;  // :293-295
+      } else if (ihl4 > 20) {
+        // ci_ip_options_parse (netif_event.c:135-185), signed-char lengths.
+        int o = l3 + 20;
+        const int end = l3 + ihl4;
+        bool err = false;
+        while (B(o) != 0u && o < end && !err) {
+          const uint32_t kind = B(o);
+          if (kind == 1u) {
+            ++o;
+          } else if (kind == 7u || kind == 68u || kind == 130u || kind == 136u) {
+            const int l = (int)(int8_t)(uint8_t)B(o + 1);
+            if (l < 4 || l > end - o) err = true;
+            else o += l;
+          } else {
+            err = true;
+          }
+        }
+        if (err) reason = OO_RX_R_IP4_OPTS_BAD;
+      }
+      if (reason == PENDING && proto == 6u && frag != 0x4000u && frag != 0u)
+        reason = OO_RX_R_TCP_SCATTERED;  // tcp_rx.c:4696-4699
+    }
+
+    if (reason == PENDING) {
+      // Demux stages in reference order (udp_rx.c:271-306,
+      // tcp_rx.c:4786-4835); the first stage with a match decides.  The
+      // first probe of every stage is loaded up front.
+      r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
+      if (proto == 17u) {
+        // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
+        // of the L3 header (udp_rx.c:157-159): bytes 16..19.
+        const uint32_t dd = N32(l3 + 16);
+        if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
+      }
+      const int nst = proto == 6u ? 3 : 2;
+      Match m = {-1, 0};
+      int stage = 0;
+      // Every stage's first slot bit, its successor's bit and the first
+      // slot's record are loaded up front (two dependent levels); the walks
+      // then usually need nothing more.
+      if (is6) {
+        const uint32_t zero[4] = {0, 0, 0, 0};
+        const uint32_t dx = r.daddr_be, sx = r.saddr_be;
+        const uint32_t mask = P.ip6_mask;
+        const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & mask;
+        const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & mask;
+        const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
+        const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
+        const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
+        const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
+        const bool o0 = occ_bit(P.occ6, h1_0), o1 = occ_bit(P.occ6, h1_1);
+        const bool o2 = nst == 3 && occ_bit(P.occ6, h1_2);
+        const bool q0 = occ_bit(P.occ6, (h1_0 + h2_0) & mask);
+        const bool q1 = occ_bit(P.occ6, (h1_1 + h2_1) & mask);
+        const bool q2 = nst == 3 && occ_bit(P.occ6, (h1_2 + h2_2) & mask);
+        Slot6 s0 = {}, s1 = {}, s2 = {};
+        if (o0) s0 = load_slot6(P, h1_0);
+        if (o1) s1 = load_slot6(P, h1_1);
+        if (o2) s2 = load_slot6(P, h1_2);
+        m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
+        stage = 1;
+        if (m.n == 0) {
+          m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
+          stage = 2;
+        }
+        if (m.n == 0 && nst == 3) {
+          m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
+          stage = 3;
+        }
+      } else {
+        const uint32_t da = r.daddr_be, sa = r.saddr_be;
+        const uint32_t mask = P.ip4_mask;
+        const uint32_t h1_0 = hash3(da, dport, sa, sport, proto) & mask;
+        const uint32_t h1_1 = hash3(da, dport, 0u, 0u, proto) & mask;
+        const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
+        const uint32_t h2_0 = hash2(da, dport, sa, sport, proto);
+        const uint32_t h2_1 = hash2(da, dport, 0u, 0u, proto);
+        const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
+        const bool o0 = occ_bit(P.occ4, h1_0), o1 = occ_bit(P.occ4, h1_1);
+        const bool o2 = nst == 3 && occ_bit(P.occ4, h1_2);
+        const bool q0 = occ_bit(P.occ4, (h1_0 + h2_0) & mask);
+        const bool q1 = occ_bit(P.occ4, (h1_1 + h2_1) & mask);
+        const bool q2 = nst == 3 && occ_bit(P.occ4, (h1_2 + h2_2) & mask);
+        Slot4 s0 = {}, s1 = {}, s2 = {};
+        if (o0) s0 = load_slot4(P, h1_0);
+        if (o1) s1 = load_slot4(P, h1_1);
+        if (o2) s2 = load_slot4(P, h1_2);
+        m = walk4(P, da, dport, sa, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
+        stage = 1;
+        if (m.n == 0) {
+          m = walk4(P, da, dport, 0u, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
+          stage = 2;
+        }
+        if (m.n == 0 && nst == 3) {
+          m = walk4(P, 0u, dport, 0u, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
+          stage = 3;
+        }
+      }
+      reason = OO_RX_R_NO_MATCH;
+      if (m.n) {
+        reason = OO_RX_R_DELIVER;
+        r.stage = (uint8_t)stage;
+        r.sock = m.first;
+        r.nmatch = (uint16_t)m.n;
+        if (m.n > 1) flags |= OO_RX_F_MULTI;
+      }
+    }
+  }
+  r.reason = (uint8_t)reason;
+  r.flags = flags;
+  Parsed ps;
+  ps.r = r;
+  ps.s4 = s4;
+  ps.pseudo = pseudo;
+  // The body sum covers window bytes [HB, span); an L4 region that ends
+  // before the frame does leaves its complement to subtract.
+  if (longl4 && E4 < span) ps.s4 -= window_sum_global(abase, E4, span);
+  ps.odd_long = (uint32_t)(shift & 1) | (longl4 ? 2u : 0u);
+  return ps;
+}
+
+// The verdict a long packet's record waited for: the window part plus the
+// body; a failure turns the record into the drop record (only the fields a
+// drop defines survive).
+__device__ __forceinline__ void finish(Parsed& ps, uint32_t body) {
+  if (!(ps.odd_long & 2u)) return;
+  uint32_t f = fold16(ps.s4 + body);
+  if (ps.odd_long & 1u) f = swap16(f);  // RFC 1071 byte-order swap
+  if (fold16(f + ps.pseudo) != 0xffffu) {
+    oo_gpu_rx_result& r = ps.r;
+    r.reason = (uint8_t)(r.proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM);
+    r.flags = (uint8_t)(r.flags & (OO_RX_F_VLAN | OO_RX_F_IP6));
+    r.stage = 0; r.l4_off = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
+    r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+  }
+}
+
+__device__ __forceinline__ void store_record(const KParams& P, uint32_t idx,
+                                             const oo_gpu_rx_result& r) {
+  uint4* o = reinterpret_cast<uint4*>(P.out + idx);
+  const uint4* src = reinterpret_cast<const uint4*>(&r);
+  o[0] = src[0];
+  o[1] = src[1];
+}
+
+// ---------------------------------------------------------------------------
+// Body streaming engine.
+//
+// The packets of a tile with bytes past the window are list positions
+// q = 0..M-1 (lane order); 8-lane group g streams q = g, g+8, ... one after
+// the other, 8 x 16 B = 128 contiguous bytes per round, so one 1-KiB piece
+// (one LDS-DMA instruction) is one round of all eight groups.  Lane (g, j)
+// holds the job at q = g + 8 j, so a group's next job is one cross-lane read
+// away.  Two cursors walk the same schedule: the issue cursor (a ring ahead,
+// with addresses) and the consume cursor; each is a few countdowns per
+// lane, so a round costs a handful of VALU ops on either side.  Each lane
+// sums its chunk (the frame's last chunk masked at the frame end) into a
+// running sum; a group's last round of a job folds the eight lanes and
+// leaves the total with lane (g, job number), where the packet's own lane
+// collects it.
+
+struct Jobs {       // a tile's jobs; lane (g, j) holds job q = g + 8 j
+  uint32_t lo, hi;  // body base: frame window byte HB
+  uint32_t nb;      // body chunks (0: no job)
+  uint32_t lim;     // frame end in window coordinates (span)
+};
+
+struct Cursor {   // this lane's view of its group's progress
+  uint32_t ik;    // the group's job number
+  uint32_t grem;  // rounds left in the group's job (0: idle)
+  uint32_t lr;    // rounds left in which this lane has a chunk
+  uint32_t nvl;   // valid bytes of this lane's last chunk of the job
+  uint64_t addr;  // this lane's next chunk (issue cursor only)
+};
+
+struct BodyAcc {
+  uint32_t acc, bs;  // running sum; the total of job gj of this lane's group
+};
+
+// The jobs of the tile whose lanes hold (abase, span): T = rounds of the
+// busiest group; myslot = the lane that will hold this lane's body sum.
+__device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t lane,
+                                           uint32_t& myslot, uint32_t& T) {
+  const int nwin = (span + 15) >> 4;
+  const uint32_t nb = nwin > HC ? (uint32_t)(nwin - HC) : 0u;
+  const uint64_t bm = __ballot(nb != 0);
+  const uint32_t M = (uint32_t)__popcll(bm);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+  const uint32_t myq = nb != 0 ? below : M + lane - below;  // a permutation of 0..63
+  myslot = (myq & 7u) * 8u + (myq >> 3);
+  const uint32_t jp = (uint32_t)__builtin_amdgcn_ds_permute((int)(myslot << 2), (int)lane);
+  const uint64_t bbase = abase + HB;
+  Jobs J;
+  J.lo = lane_get((uint32_t)bbase, jp);
+  J.hi = lane_get((uint32_t)(bbase >> 32), jp);
+  J.nb = lane_get(nb, jp);  // 0 past the list
+  J.lim = lane_get((uint32_t)span, jp);
+  const uint32_t gr = group_sum8((J.nb + 7u) >> 3);
+  T = (uint32_t)__builtin_amdgcn_readlane((int)gr, 0);
+#pragma unroll
+  for (int g = 1; g < 8; ++g) T = max(T, (uint32_t)__builtin_amdgcn_readlane((int)gr, 8 * g));
+  return J;
+}
+
+// Point the cursor at job k of its group (k >= 8: done).  All lanes active.
+template <bool ADDR>
+__device__ __forceinline__ void cursor_job(Cursor& c, const Jobs& J, uint32_t k, uint32_t lane) {
+  const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(k, 7u);
+  const uint32_t nbs = lane_get(J.nb, s), lim = lane_get(J.lim, s);
+  const uint32_t nb = k < 8u ? nbs : 0u;
+  c.ik = k;
+  c.grem = (nb + 7u) >> 3;
+  c.lr = nb > gj ? (nb - gj + 7u) >> 3 : 0u;
+  const int last_pos = HB + 16 * (int)(gj + 8u * (c.lr - 1u));  // this lane's last chunk
+  c.nvl = (uint32_t)min(max((int)lim - last_pos, 0), 16);
+  if (ADDR) c.addr = ((uint64_t)lane_get(J.hi, s) << 32 | lane_get(J.lo, s)) + gj * 16u;
+}
+
+// One round done: count down; groups whose job ended move to their next.
+template <bool ADDR>
+__device__ __forceinline__ void cursor_step(Cursor& c, const Jobs& J, uint32_t lane) {
+  const bool had = c.grem != 0;
+  c.lr -= c.lr != 0 ? 1u : 0u;
+  if (ADDR) c.addr += 128;
+  c.grem -= had ? 1u : 0u;
+  const bool next = had && c.grem == 0;
+  if (__ballot(next) != 0) {
+    Cursor n;
+    cursor_job<ADDR>(n, J, c.ik + 1, lane);
+    if (next) c = n;
+  }
+}
+
+// Issues the cursor's round into `slot` (lanes without a chunk read `spare`).
+__device__ __forceinline__ void issue_round(Cursor& c, const Jobs& J, uint64_t spare, void* slot,
+                                            uint32_t lane) {
+  glds<OO_RX_BODY_AUX>(c.lr != 0 ? c.addr : spare, slot);
+  cursor_step<true>(c, J, lane);
+}
+
+// Consumes the cursor's round from the landed bytes v.
+__device__ __forceinline__ void consume_round(Cursor& c, const Jobs& J, const uint4& v, BodyAcc& a,
+                                              uint32_t lane) {
+  const bool live = c.lr != 0;
+  const uint32_t nv = live ? (c.lr == 1u ? c.nvl : 16u) : 0u;
+  uint32_t s;
+  if (__ballot(nv != 16u && nv != 0u) == 0) {  // whole or no chunks only (wave-uniform)
+    s = chunk_sum_all(v, 0u);
+    s = live ? s : 0u;
+  } else {
+    s = nv == 16u ? chunk_sum_all(v, 0u) : (nv != 0u ? chunk_sum(v, 0, 0, (int)nv) : 0u);
+  }
+  a.acc += s;
+  if (__ballot(c.grem == 1u) != 0) {  // some group's job ends this round
+    const uint32_t t = group_sum8(a.acc);
+    if (c.grem == 1u) {
+      if ((lane & 7u) == c.ik) a.bs = t;
+      a.acc = 0;
+    }
+  }
+  cursor_step<false>(c, J, lane);
+}
+
 // ---------------------------------------------------------------------------
 
-#if OO_RX_WPE > 0
-#define OO_RX_KATTR __attribute__((amdgpu_waves_per_eu(OO_RX_WPE)))
-#else
-#define OO_RX_KATTR
-#endif
+// A tile's descriptor as seen by its lane: frame start, its 16-B-aligned base
+// and span, all 0 for lanes without a packet or out-of-buffer descriptors.
+struct DescView {
+  uint64_t abase;
+  int shift, len, span, intf_i;
+  bool valid;
+  uint32_t idx;
+};
+__device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, uint32_t tile,
+                                              uint32_t lane) {
+  DescView v;
+  v.idx = tile * P.tile + lane;
+  v.valid = lane < P.tile && v.idx < P.n;
+  const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
+  int len = (int)(d.z & 0xffffu);
+  v.intf_i = (int)(int16_t)(d.z >> 16);
+  const bool inb = v.valid && off + (uint64_t)len <= P.frames_bytes;
+  if (!inb) len = 0;  // a descriptor outside the buffer is an empty frame
+  const uint64_t base = reinterpret_cast<uint64_t>(P.frames) + (inb ? off : 0);
+  v.shift = (int)(base & 15u);
+  v.abase = base - (uint64_t)v.shift;
+  v.len = len;
+  v.span = inb ? v.shift + len : 0;
+  return v;
+}
 
-// Per-wave LDS.  All LDS lives in one __shared__ array (a second __shared__
-// object can make hipcc wait vmcnt(0) before LDS reads while LDS-DMA is in
-// flight).
+// A lane that has nothing to load still issues its part of an LDS-DMA
+// instruction (so every instruction is issued by the whole wave and the
+// counted waits stay static); it reads this line instead: its own entry of
+// the descriptor array, which the tile has just brought into L2.  (One
+// common dummy line for every wave of the GPU made a hot spot on one L2
+// channel.)
+__device__ __forceinline__ uint64_t spare_line(const KParams& P, uint32_t tile, uint32_t lane) {
+  return reinterpret_cast<uint64_t>(P.desc) + (uint64_t)((tile * P.tile + lane) % P.n) * 16;
+}
+
+__device__ __forceinline__ uint64_t desc_src(const KParams& P, uint32_t tile, uint32_t lane,
+                                             uint32_t ntiles) {
+  const uint32_t i = tile * P.tile + lane;
+  return reinterpret_cast<uint64_t>(P.desc) +
+         (uint64_t)((tile < ntiles && lane < P.tile && i < P.n) ? i : lane % P.n) * 16;
+}
+
+// Per-reason counters: one global atomic per distinct reason in the wave
+// (usually one or two per tile).  Not LDS: see parse_tile.
+__device__ __forceinline__ void count_reasons(const KParams& P, bool valid, uint32_t reason) {
+  if (P.counters == nullptr) return;
+  uint64_t left = __ballot(valid);
+  while (left != 0) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(left);
+    const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)reason, (int)first);
+    const uint64_t same = __ballot(valid && reason == r) & left;
+    if ((threadIdx.x & 63u) == first)
+      atomicAdd(&P.counters[r & (OO_RX_R_COUNT - 1)], (uint32_t)__popcll(same));
+    left &= ~same;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// rx_kernel: every wave parses and streams its own tiles.
+
 struct WaveLds {
-  uint4 hdr[HC][64];   // header window, [chunk][packet] 16-B cells
-  uint4 ring[R][64];   // body ring: slot = one round of the eight groups
-  uint4 desc[64];      // the tile's descriptors
+  uint4 hdr[HC][64];  // header window, [chunk][packet] 16-B cells
+  uint4 ring[R][64];  // body ring: slot = one round of the eight groups
+  uint4 desc[64];     // the tile's descriptors
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
 constexpr int WAVE_U4 = (int)(sizeof(WaveLds) / 16);
 
-__global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES * WAVE_U4 + OO_RX_R_COUNT / 4];
+__global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
+  // All LDS in one __shared__ array (a second object can make hipcc wait
+  // vmcnt(0) before LDS reads while LDS-DMA is in flight).
+  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES * WAVE_U4];
 
   const int wave = (int)(threadIdx.x >> 6);
-  const int lane = (int)(threadIdx.x & 63);
-  const uint32_t grp = (uint32_t)lane >> 3;  // 8-lane group
-  const uint32_t gj = (uint32_t)lane & 7u;   // lane within the group
+  const uint32_t lane = threadIdx.x & 63u;
   WaveLds& L = reinterpret_cast<WaveLds*>(smem)[wave];
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + WAVES * WAVE_U4);
-  if (threadIdx.x < OO_RX_R_COUNT) ctr[threadIdx.x] = 0;
-  __syncthreads();
 
-  // Tiles of P.tile packets (<= 64), sized by the host so that every wave
-  // gets the same number of tiles (oo_gpu_rx.cpp launch()).
-  const uint32_t TS = P.tile;
-  const uint32_t ntiles = (P.n + TS - 1) / TS;
+  const uint32_t ntiles = (P.n + P.tile - 1) / P.tile;
   const uint32_t stride = gridDim.x * WAVES;
   uint32_t tile = blockIdx.x * WAVES + wave;
-  // Lanes with nothing to load read this always-mapped 16-B line instead, so
+  // Lanes with nothing to load read this always-mapped line instead, so
   // every LDS-DMA instruction is issued by the whole wave and the counted
   // waits stay static.
-  const uint64_t dummy = reinterpret_cast<uint64_t>(P.desc);
-  const uint64_t descs = reinterpret_cast<uint64_t>(P.desc);
-  auto issue_desc = [&](uint32_t t) {
-    const uint32_t i = t * TS + (uint32_t)lane;
-    glds((uint32_t)lane < TS && i < P.n ? descs + (uint64_t)i * 16 : dummy, &L.desc[0]);
-  };
-  if (tile < ntiles) issue_desc(tile);
+  if (tile < ntiles) glds<0>(desc_src(P, tile, lane, ntiles), &L.desc[0]);
   vm_wait<0>();
   const uint32_t gwave = blockIdx.x * WAVES + wave;
   uint32_t it_ = 0;
@@ -381,485 +874,310 @@ __global__ __launch_bounds__(WAVES * 64) OO_RX_KATTR void rx_kernel(KParams P) {
   for (; tile < ntiles; tile += stride, ++it_) {
     STAMP(0, __builtin_amdgcn_s_memrealtime());
     STAMP(6, tile);
-    // ---- 1. descriptor (landed: every earlier wait retired it), then the
-    // next tile's.
-    const uint32_t idx = tile * TS + (uint32_t)lane;
-    const bool valid = (uint32_t)lane < TS && idx < P.n;
+    // ---- 1. descriptors (landed: every earlier wait retired them), then
+    // the next tile's.
     const uint4 d = lds_read16(&L.desc[lane]);
-    if (tile + stride < ntiles) issue_desc(tile + stride);
-    const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
-    int len = (int)(d.z & 0xffffu);
-    const int intf_i = (int)(int16_t)(d.z >> 16);
-    const bool inb = valid && off + (uint64_t)len <= P.frames_bytes;
-    if (!inb) len = 0;  // a descriptor outside the buffer is an empty frame
-    const uint64_t base = reinterpret_cast<uint64_t>(P.frames) + (inb ? off : 0);
-    const int shift = (int)(base & 15u);
-    const uint64_t abase = base - (uint64_t)shift;
-    const int span = inb ? shift + len : 0;
-    const int nwin = (span + 15) >> 4;  // 16-B chunks the frame touches
+    if (tile + stride < ntiles) glds<0>(desc_src(P, tile + stride, lane, ntiles), &L.desc[0]);
+    const DescView dv = desc_view(P, d, tile, lane);
+    const uint64_t spare = spare_line(P, tile, lane);
+    const int nwin = (dv.span + 15) >> 4;
 
     // ---- 2. header window: chunk k of every frame, lane = packet.
 #pragma unroll
-    for (int k = 0; k < HC; ++k) glds<OO_RX_HDR_AUX>(k < nwin ? abase + (uint64_t)k * 16 : dummy, &L.hdr[k][0]);
+    for (int k = 0; k < HC; ++k)
+      glds<OO_RX_HDR_AUX>(k < nwin ? dv.abase + (uint64_t)k * 16 : spare, &L.hdr[k][0]);
 
-    // ---- 3. body jobs.  The packets with chunks past the window, in lane
-    // order, are list positions q = 0..M-1; group g takes q = g, g+8, ...
-    // Lane (g, j) holds the job at q = g + 8 j (a permutation, so every lane
-    // sends and receives exactly one value).
-    const uint32_t nb = nwin > HC ? (uint32_t)(nwin - HC) : 0u;
-    const uint64_t bm = __ballot(nb != 0);
-    const uint32_t M = (uint32_t)__popcll(bm);
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-    const uint32_t myq = nb != 0 ? below : M + (uint32_t)lane - below;
-    const uint32_t myslot = (myq & 7u) * 8u + (myq >> 3);  // lane holding job myq
-    const uint32_t jp = (uint32_t)__builtin_amdgcn_ds_permute((int)(myslot << 2), lane);
-    const uint64_t bbase = abase + HB;
-    const uint32_t jlo = lane_get((uint32_t)bbase, jp);
-    const uint32_t jhi = lane_get((uint32_t)(bbase >> 32), jp);
-    const uint32_t jnb = lane_get(nb, jp);  // 0 for lanes past the list
-    // Rounds of the body stream = the busiest group's.
-    const uint32_t gr = group_sum8((jnb + 7u) >> 3);
-    uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)gr, 0);
+    // ---- 3. body jobs; the first R rounds land during the parse.
+    uint32_t myslot, T;
+    const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot, T);
+    T = (T + R - 1) / R * R;  // whole ring turns; the padding rounds are idle
+    Cursor ci, cc;
+    cursor_job<true>(ci, J, 0, lane);
+    cc = ci;
+    if (T != 0) {
 #pragma unroll
-    for (int g = 1; g < 8; ++g) T = max(T, (uint32_t)__builtin_amdgcn_readlane((int)gr, 8 * g));
-
-    // Issue state: the group's job number ik, its packet ip, this lane's
-    // chunk ic (= 8 * round + gj) out of inb_, and the source address.
-    const uint32_t gsrc = grp * 8u;
-    uint32_t ik = 0;
-    uint32_t ip = lane_get(jp, gsrc), inb_ = lane_get(jnb, gsrc), ic = gj;
-    uint64_t iaddr = ((uint64_t)lane_get(jhi, gsrc) << 32 | lane_get(jlo, gsrc)) + gj * 16u;
-    // Per piece (slot u) and lane, meta[u] says what landed: before the
-    // parse, {packet, chunk, live, last}; after it, {valid bytes nv (0..16)
-    // of the chunk inside the packet's summed region, last}.
-    uint32_t meta[R];
-    uint32_t ilim = 0;  // summed-region end of the job being issued (after the parse)
-    uint32_t lim_mine = HB;
-    auto advance = [&](bool last, bool post) {
-      ic += 8;
-      iaddr += 128;
-      if (__ballot(last) != 0) {  // some group moves to its next job
-        const uint32_t s = gsrc + min(ik + 1, 7u);
-        const uint32_t np = lane_get(jp, s), nnb = lane_get(jnb, s);
-        const uint32_t nlo = lane_get(jlo, s), nhi = lane_get(jhi, s);
-        const uint32_t nlim = post ? lane_get(lim_mine, np) : 0u;
-        if (last) {
-          ++ik;
-          ip = np;
-          inb_ = ik < 8u ? nnb : 0u;
-          ic = gj;
-          iaddr = ((uint64_t)nhi << 32 | nlo) + gj * 16u;
-          ilim = nlim;
-        }
-      }
-    };
-    auto issue_pre = [&](int u) {
-      const bool live = ic < inb_;
-      glds<OO_RX_BODY_AUX>(live ? iaddr : dummy, &L.ring[u][0]);
-      const bool last = inb_ != 0 && ic - gj + 8 >= inb_;
-      meta[u] = ip | (ic << 6) | (live ? M_LIVE : 0u) | (last ? M_LAST : 0u);
-      advance(last, false);
-    };
-    auto issue = [&](int u) {
-      const bool live = ic < inb_;
-      glds<OO_RX_BODY_AUX>(live ? iaddr : dummy, &L.ring[u][0]);
-      const bool last = inb_ != 0 && ic - gj + 8 >= inb_;
-      const int nv = live ? min(max((int)ilim - (HB + 16 * (int)ic), 0), 16) : 0;
-      meta[u] = (uint32_t)nv | (last ? M_LAST : 0u);
-      advance(last, true);
-    };
-
-    // Body prologue (lands during the parse), then wait for the header window.
-#ifdef OO_RX_EXP_LATEPRO
-    if (false) {
-#else
-    if (T >= (uint32_t)R) {
-#endif
-#pragma unroll
-      for (int u = 0; u < R; ++u) issue_pre(u);
-      vm_wait<R>();
+      for (int u = 0; u < R; ++u) issue_round(ci, J, spare, &L.ring[u][0], lane);
+      vm_wait<R>();  // the header window (and the next descriptors)
     } else {
-#pragma unroll
-      for (int u = 0; u < R; ++u) {
-        if ((uint32_t)u < T) issue_pre(u);
-        else meta[u] = 0;
-      }
       vm_wait<0>();
     }
     STAMP(1, __builtin_amdgcn_s_memrealtime());
     STAMP(7, T);
 
-    const uint8_t* my = reinterpret_cast<const uint8_t*>(&L.hdr[0][lane]);
-    // Header byte j (j >= 0); bytes at or beyond the frame length read 0.
-    auto B = [&](int j) -> uint32_t {
-      int w = shift + j;
-      w = w < HB ? w : HB - 1;
-      const uint32_t v = my[(w >> 4) * ROWB + (w & 15)];
-      return j < len ? v : 0u;
-    };
-    auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
-    auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
-    auto N32 = [&](int j) -> uint32_t { return N16(j) | (N16(j + 2) << 16); };
-
-#ifdef OO_RX_EXP_STREAMONLY
-    // Experiment build: no parse/demux; every frame's bytes past the window
-    // are summed (timing of the stream machinery alone; records are garbage).
-    oo_gpu_rx_result r;
-    __builtin_memset(&r, 0, sizeof(r));
-    const bool longl4 = span > HB;
-    const int E4 = span;
-    uint32_t s4 = 0, pseudo = 1;
-    const uint32_t proto = 17, flags = 0;
-#else
-    // ---- 4. parse (per lane)
-    uint8_t flags = 0;
-    int pre_l3 = 14, vlan = 0;
-    if (BE16(12) == 0x8100u) {  // ci_parse_rx_vlan (netif_event.c:116-132)
-      pre_l3 = 18;
-      vlan = (int)(BE16(14) & 0xfffu);
-      flags |= OO_RX_F_VLAN;
-    }
-    const int l3 = pre_l3;
-    uint32_t reason = PENDING;
-    bool is6 = false, l3ok = false;
-    int ip_len = 0, ihl4 = 0, ip_paylen = 0, l4 = 0;
-    uint32_t proto = 0;
-    if (len < pre_l3 + 20) {  // netif_event.c:1030
-      reason = OO_RX_R_SHORT_L2;
-    } else {
-      const uint32_t et = BE16(pre_l3 - 2);
-      if (et == 0x0800u) {  // :1038-1058
-        l3ok = true;
-        ip_len = (int)BE16(l3 + 2);
-        ihl4 = (int)(B(l3) & 0xfu) * 4;
-        ip_paylen = ip_len - ihl4;
-        proto = B(l3 + 9);
-        if (ip_paylen <= 0 || len < pre_l3 + ip_len) reason = OO_RX_R_IP4_LEN;
-        l4 = l3 + ihl4;
-      } else if (et == 0x86ddu) {  // :1060-1076
-        l3ok = true;
-        is6 = true;
-        flags |= OO_RX_F_IP6;
-        ip_paylen = (int)BE16(l3 + 4);
-        proto = B(l3 + 6);
-        if (ip_paylen <= 0 || len < pre_l3 + 40 + ip_paylen) reason = OO_RX_R_IP6_LEN;
-        l4 = l3 + 40;
-      } else {
-        reason = OO_RX_R_NOT_IP;  // :1078
-      }
-    }
-
-    // L4 gates (netif_event.c:1084-1127) -> which region to sum.
-    uint32_t l4_gate = PENDING;
-    bool need_l4 = false;
-    int l4_len = 0;
-    uint32_t pseudo = 0;
-    if (reason == PENDING) {
-      if (proto == 6u) {
-        const int hlen = (int)((B(l4 + 12) & 0xf0u) >> 2);
-        if (ip_paylen < 20) l4_gate = OO_RX_R_TCP_SHORT;
-        else if (hlen < 20 || ip_paylen < hlen) l4_gate = OO_RX_R_TCP_CSUM;
-        else { need_l4 = true; l4_len = ip_paylen; }
-      } else if (proto == 17u) {
-        const uint32_t udp_len = BE16(l4 + 4);
-        if (ip_paylen < 8) l4_gate = OO_RX_R_UDP_SHORT;
-        else if (udp_len < 8u || udp_len > (uint32_t)ip_paylen) l4_gate = OO_RX_R_UDP_CSUM;
-        else if (!(N16(l4 + 6) == 0u && !is6)) { need_l4 = true; l4_len = (int)udp_len; }
-      } else {
-        l4_gate = OO_RX_R_PROTO_OTHER;
-      }
-      if (need_l4) {
-        // Pseudo-header words (checksum.c:215-223, 304-305, 334-335).
-        if (is6) {
-          uint32_t a = 0;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) a += N16(l3 + 8 + 2 * i);
-          pseudo = a + (proto == 6u ? N16(l3 + 4) + 0x0600u : N16(l4 + 4) + 0x1100u);
-        } else {
-          pseudo = N16(l3 + 12) + N16(l3 + 14) + N16(l3 + 16) + N16(l3 + 18);
-          if (proto == 6u) {
-            const uint32_t pl = (uint32_t)ip_paylen & 0xffffu;
-            pseudo += 0x0600u + (((pl & 0xffu) << 8) | (pl >> 8));
-          } else {
-            pseudo += 0x1100u + N16(l4 + 4);
-          }
-        }
-      }
-    }
-
-    // Sums over the staged window: IPv4 header [S3,E3), L4 head [S4,min(E4,HB)).
-    const bool need_ip = reason == PENDING && !is6;
-    const int S3 = shift + l3, E3 = need_ip ? shift + l3 + ihl4 : S3;
-    const int S4 = shift + l4, E4 = need_l4 ? shift + l4 + l4_len : S4;
-    const int E4h = E4 < HB ? E4 : HB;
-    uint32_t s3 = 0, s4 = 0;
-    if (need_ip || need_l4) {
-#pragma unroll
-      for (int k = 0; k < HC; ++k) {
-        const uint4 v = *reinterpret_cast<const uint4*>(my + k * ROWB);
-        if (k * 16 < E3) s3 += chunk_sum(v, k * 16, S3, E3);
-        if (k * 16 < E4h) s4 += chunk_sum(v, k * 16, S4, E4h);
-      }
-    }
-    if (reason == PENDING && need_ip) {
-      // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
-      if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
-    }
-    if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
-
-    // L4 verdict now when the region ends inside the window; otherwise it
-    // waits for the body stream (step 5) and the record below is speculative.
-    const bool longl4 = reason == PENDING && need_l4 && E4 > HB;
-    if (reason == PENDING && need_l4 && !longl4) {
-      uint32_t f = fold16(s4);
-      if (shift & 1) f = swap16(f);  // RFC 1071 byte-order swap
-      if (fold16(f + pseudo) != 0xffffu)
-        reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
-    }
-
-    STAMP(2, __builtin_amdgcn_s_memrealtime());
-    // ---- handle_rx_pkt, demux, record (per lane; netif_event.c:250-451).
-    oo_gpu_rx_result r;
-    r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
-    r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
-    r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
-    if (l3ok) {
-      r.proto = (uint8_t)proto;
-      r.ip_paylen = (uint16_t)ip_paylen;
-    }
-    if (reason == PENDING) {
-      flags |= OO_RX_F_CSUM_OK;
-      r.l4_off = (uint16_t)l4;
-      const uint32_t sport = N16(l4), dport = N16(l4 + 2);
-      r.sport_be = (uint16_t)sport;
-      r.dport_be = (uint16_t)dport;
-      uint32_t a6s[4], a6d[4];
-      if (is6) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          a6s[i] = N32(l3 + 8 + 4 * i);
-          a6d[i] = N32(l3 + 24 + 4 * i);
-        }
-        r.saddr_be = a6s[0] ^ a6s[1] ^ a6s[2] ^ a6s[3];
-        r.daddr_be = a6d[0] ^ a6d[1] ^ a6d[2] ^ a6d[3];
-      } else {
-        r.saddr_be = N32(l3 + 12);
-        r.daddr_be = N32(l3 + 16);
-        const uint32_t frag = BE16(l3 + 6);
-        if ((frag & 0x3fffu) != 0 || ip_len > len - pre_l3) {
-          reason = OO_RX_R_IP4_FRAG;  // :293-295
-        } else if (ihl4 > 20) {
-          // ci_ip_options_parse (netif_event.c:135-185), signed-char lengths.
-          int o = l3 + 20;
-          const int end = l3 + ihl4;
-          bool err = false;
-          while (B(o) != 0u && o < end && !err) {
-            const uint32_t kind = B(o);
-            if (kind == 1u) {
-              ++o;
-            } else if (kind == 7u || kind == 68u || kind == 130u || kind == 136u) {
-              const int l = (int)(int8_t)(uint8_t)B(o + 1);
-              if (l < 4 || l > end - o) err = true;
-              else o += l;
-            } else {
-              err = true;
-            }
-          }
-          if (err) reason = OO_RX_R_IP4_OPTS_BAD;
-        }
-        if (reason == PENDING && proto == 6u && frag != 0x4000u && frag != 0u)
-          reason = OO_RX_R_TCP_SCATTERED;  // tcp_rx.c:4696-4699
-      }
-
-      if (reason == PENDING) {
-        // Demux stages in reference order (udp_rx.c:271-306,
-        // tcp_rx.c:4786-4835); the first stage with a match decides.  The
-        // first probe of every stage is loaded up front.
-        r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
-        if (proto == 17u) {
-          // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
-          // of the L3 header (udp_rx.c:157-159): bytes 16..19.
-          const uint32_t dd = N32(l3 + 16);
-          if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
-        }
-        const int nst = proto == 6u ? 3 : 2;
-        Match m = {-1, 0};
-        int stage = 0;
-        // Every stage's first slot bit, its successor's bit and the first
-        // slot's record are loaded up front (two dependent levels); the walks
-        // then usually need nothing more.
-        if (is6) {
-          const uint32_t zero[4] = {0, 0, 0, 0};
-          const uint32_t dx = r.daddr_be, sx = r.saddr_be;
-          const uint32_t mask = P.ip6_mask;
-          const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & mask;
-          const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & mask;
-          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
-          const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
-          const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
-          const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
-          const bool o0 = occ_bit(P.occ6, h1_0), o1 = occ_bit(P.occ6, h1_1);
-          const bool o2 = nst == 3 && occ_bit(P.occ6, h1_2);
-          const bool q0 = occ_bit(P.occ6, (h1_0 + h2_0) & mask);
-          const bool q1 = occ_bit(P.occ6, (h1_1 + h2_1) & mask);
-          const bool q2 = nst == 3 && occ_bit(P.occ6, (h1_2 + h2_2) & mask);
-          Slot6 s0 = {}, s1 = {}, s2 = {};
-          if (o0) s0 = load_slot6(P, h1_0);
-          if (o1) s1 = load_slot6(P, h1_1);
-          if (o2) s2 = load_slot6(P, h1_2);
-          m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
-          stage = 1;
-          if (m.n == 0) {
-            m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
-            stage = 2;
-          }
-          if (m.n == 0 && nst == 3) {
-            m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
-            stage = 3;
-          }
-        } else {
-          const uint32_t da = r.daddr_be, sa = r.saddr_be;
-          const uint32_t mask = P.ip4_mask;
-          const uint32_t h1_0 = hash3(da, dport, sa, sport, proto) & mask;
-          const uint32_t h1_1 = hash3(da, dport, 0u, 0u, proto) & mask;
-          const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
-          const uint32_t h2_0 = hash2(da, dport, sa, sport, proto);
-          const uint32_t h2_1 = hash2(da, dport, 0u, 0u, proto);
-          const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
-          const bool o0 = occ_bit(P.occ4, h1_0), o1 = occ_bit(P.occ4, h1_1);
-          const bool o2 = nst == 3 && occ_bit(P.occ4, h1_2);
-          const bool q0 = occ_bit(P.occ4, (h1_0 + h2_0) & mask);
-          const bool q1 = occ_bit(P.occ4, (h1_1 + h2_1) & mask);
-          const bool q2 = nst == 3 && occ_bit(P.occ4, (h1_2 + h2_2) & mask);
-          Slot4 s0 = {}, s1 = {}, s2 = {};
-          if (o0) s0 = load_slot4(P, h1_0);
-          if (o1) s1 = load_slot4(P, h1_1);
-          if (o2) s2 = load_slot4(P, h1_2);
-          m = walk4(P, da, dport, sa, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
-          stage = 1;
-          if (m.n == 0) {
-            m = walk4(P, da, dport, 0u, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
-            stage = 2;
-          }
-          if (m.n == 0 && nst == 3) {
-            m = walk4(P, 0u, dport, 0u, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
-            stage = 3;
-          }
-        }
-        reason = OO_RX_R_NO_MATCH;
-        if (m.n) {
-          reason = OO_RX_R_DELIVER;
-          r.stage = (uint8_t)stage;
-          r.sock = m.first;
-          r.nmatch = (uint16_t)m.n;
-          if (m.n > 1) flags |= OO_RX_F_MULTI;
-        }
-      }
-    }
-    r.reason = (uint8_t)reason;
-    r.flags = flags;
-#endif
-
-
-
-    // ---- 5. body stream.  Each lane sums its chunk, masked at the L4 region
-    // end (lim of its packet); on a group's last round of a packet the 8-lane
-    // total goes to lane (g, job number), whose packet lane collects it
-    // below.  Packets whose verdict is already final sum nothing (lim = HB).
-#ifdef OO_RX_EXP_LATEPRO
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      if ((uint32_t)u < T) issue_pre(u);
-      else meta[u] = 0;
-    }
-#endif
-    lim_mine = longl4 ? (uint32_t)E4 : (uint32_t)HB;
-    ilim = lane_get(lim_mine, ip);
-#pragma unroll
-    for (int u = 0; u < R; ++u) {  // the prologue's meta, now that lim is known
-      const uint32_t mt = meta[u];
-      const int lim = (int)lane_get(lim_mine, mt & 63u);
-      const int nv = min(max(lim - (HB + 16 * (int)((mt >> 6) & 1023u)), 0), 16);
-      meta[u] = (mt & M_LIVE ? (uint32_t)nv : 0u) | (mt & M_LAST);
-    }
-    uint32_t acc = 0, bs = 0, ck = 0;
-    auto consume = [&](int u) {
-      const uint32_t mt = meta[u];
-      const uint4 v = lds_read16(&L.ring[u][lane]);
-      const int nv = (int)(mt & 31u);
-      if (nv == 16) acc = chunk_sum_all(v, acc);
-      else if (nv != 0) acc += chunk_sum(v, 0, 0, nv);
-      if (__ballot((mt & M_LAST) != 0) != 0) {
-        const uint32_t t = group_sum8(acc);
-        if (mt & M_LAST) {
-          if (gj == ck) bs = t;
-          ++ck;
-          acc = 0;
-        }
-      }
-    };
+    // ---- 4. header work (one packet per lane).
+    Parsed ps = parse_packet<ROWB>(P, reinterpret_cast<const uint8_t*>(&L.hdr[0][lane]), dv.shift,
+                                   dv.len, dv.intf_i, dv.abase, dv.span);
     STAMP(3, __builtin_amdgcn_s_memrealtime());
+
+    // ---- 5. body stream (T is a multiple of R).
+    BodyAcc ba = {0, 0};
+    // Two pieces per step: one wait and one LDS round trip per 2 KiB.
     for (uint32_t k0 = 0; k0 < T; k0 += R) {
 #pragma unroll
-      for (int u = 0; u < R; ++u) {
+      for (int u = 0; u < R; u += 2) {
         const uint32_t k = k0 + (uint32_t)u;
-        if (k < T) {
-          // Pieces k+1 .. min(T, k+R)-1 may still be in flight.
-          if (k + R <= T) vm_wait<R - 1>();
-          else vm_wait<0>();
-          consume(u);
-          if (k + R < T) issue(u);  // slot u was read (lds_read16 waited)
+        // Pieces k+2 .. min(T, k+R)-1 may still be in flight.
+        if (k + R <= T) vm_wait<R - 2>();
+        else vm_wait<0>();
+        uint4 v0, v1;
+        lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
+        consume_round(cc, J, v0, ba, lane);
+        consume_round(cc, J, v1, ba, lane);
+        if (k + R < T) {
+          issue_round(ci, J, spare, &L.ring[u][0], lane);
+          issue_round(ci, J, spare, &L.ring[u + 1][0], lane);
         }
       }
     }
-    const uint32_t body = lane_get(bs, myslot);
     STAMP(4, __builtin_amdgcn_s_memrealtime());
 
-    if (longl4) {
-      // The verdict the speculative record waited for; a failure turns it
-      // into the drop record (only the fields a drop defines survive).
-      s4 += body;
-      uint32_t f = fold16(s4);
-      if (shift & 1) f = swap16(f);
-      if (fold16(f + pseudo) != 0xffffu) {
-        r.reason = (uint8_t)(proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM);
-        r.flags = (uint8_t)(flags & (OO_RX_F_VLAN | OO_RX_F_IP6));
-        r.stage = 0; r.l4_off = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
-        r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
-      }
-    }
-
-    if (valid) {
-      atomicAdd(&ctr[r.reason & (OO_RX_R_COUNT - 1)], 1u);
-      uint4* o = reinterpret_cast<uint4*>(P.out + idx);
-      const uint4* src = reinterpret_cast<const uint4*>(&r);
-      o[0] = src[0];
-      o[1] = src[1];
-    }
+    finish(ps, lane_get(ba.bs, myslot));
+    count_reasons(P, dv.valid, ps.r.reason);
+    if (dv.valid) store_record(P, dv.idx, ps.r);
     STAMP(5, __builtin_amdgcn_s_memrealtime());
   }
+}
 
-  __syncthreads();
-  if (P.counters != nullptr && threadIdx.x < OO_RX_R_COUNT && ctr[threadIdx.x] != 0)
-    atomicAdd(&P.counters[threadIdx.x], ctr[threadIdx.x]);
+// ---------------------------------------------------------------------------
+// rx_split: one parser wave + WS streamer waves per block.
+//
+// Tile phase k of block b gives streamer i the tile (k * G + b) * WS + i.
+// In phase k each streamer streams the body of its phase-k tile while the
+// parser parses all WS of them and finalises the phase k-1 tiles, whose
+// body sums the streamers left in LDS before the barrier that ends phase
+// k-1.  A streamer's ring runs on across tiles and barriers: once its tile's
+// pieces are all issued it issues the next tile's (its descriptors are
+// fetched two phases ahead), so the stream never drains.  The parser uses
+// no LDS-DMA: its loads and LDS accesses are ordinary ones.
+
+struct StreamerLds {
+  uint4 ring[SR][64];    // body ring
+  uint4 desc[3][64];     // descriptors of tiles k, k+1, k+2 (by tile phase mod 3)
+  uint32_t bsum[2][64];  // body sums of a finished tile, by phase parity
+};
+struct SplitLds {
+  StreamerLds s[WS];
+  uint4 hdr[HC][64];  // the parser's header window, [chunk][packet]
+};
+static_assert(SR >= 2 && SR % 2 == 0, "a streamer consumes its ring two pieces at a time");
+
+__device__ __forceinline__ void lds_write4(void* p, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void block_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// The parser's header work for tile t: the window staged by LDS-DMA (lane
+// = packet, [chunk][packet] cells, as in rx_kernel), then the common parse.
+__device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (&hdr)[HC][64], uint32_t t,
+                                             uint32_t lane) {
+  const uint32_t idx = t * P.tile + lane;
+  uint4 d = make_uint4(0, 0, 0, 0);
+  if (lane < P.tile && idx < P.n) d = *reinterpret_cast<const uint4*>(P.desc + idx);
+  const DescView dv = desc_view(P, d, t, lane);
+  // LDS-DMA staging, lane = packet, [chunk][packet] cells.
+  const int nwin = (dv.span + 15) >> 4;
+#pragma unroll
+  for (int k = 0; k < HC; ++k)
+    glds<OO_RX_HDR_AUX>(k < nwin ? dv.abase + (uint64_t)k * 16 : spare_line(P, t, lane), &hdr[k][0]);
+  vm_wait<0>();
+  return parse_packet<ROWB>(P, reinterpret_cast<const uint8_t*>(&hdr[0][lane]), dv.shift, dv.len,
+                            dv.intf_i, dv.abase, dv.span);
+}
+
+__global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[(sizeof(SplitLds) + 15) / 16];
+  SplitLds& L = *reinterpret_cast<SplitLds*>(smem);
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t ntiles = (P.n + P.tile - 1) / P.tile;
+  const uint32_t G = gridDim.x;
+  const uint32_t K = (ntiles + G * WS - 1) / (G * WS);  // tile phases
+  auto tile_of = [&](uint32_t k, uint32_t i) { return (k * G + blockIdx.x) * WS + i; };
+#ifdef OO_RX_STAMPS
+  // Diagnostic: stamps[((block * (WS + 1) + wave) * 64 + phase) * 8 + slot].
+  auto sstamp = [&](uint32_t k, int ph, uint64_t val) {
+    if (P.stamps != nullptr && lane == 0 && k < 64)
+      P.stamps[(((size_t)blockIdx.x * (WS + 1) + wave) * 64 + k) * 8 + ph] = val;
+  };
+#define SSTAMP(k, ph) sstamp((k), (ph), __builtin_amdgcn_s_memrealtime())
+#else
+#define SSTAMP(k, ph) \
+  do {                \
+  } while (0)
+#endif
+
+  if (wave < (uint32_t)WS) {
+    // ---------------- streamer
+    //
+    // The ring is always full: every slot is refilled as soon as it is
+    // read, with the issue cursor's next round or, when the issue side may
+    // not run further ahead (it stays at most one tile ahead of the consume
+    // side, and stops after the last tile), with a null piece that the
+    // consume side skips.  Slots are static (the loop is unrolled over the
+    // ring), so every wait is the same vmcnt(SR-2).
+    StreamerLds& S = L.s[wave];
+    const uint32_t i = wave;
+    glds<0>(desc_src(P, tile_of(0, i), lane, ntiles), &S.desc[0][0]);
+    vm_wait<0>();
+
+    // issue side: tile ti, its jobs and cursor
+    uint32_t ti = 0, Ti = 0, issued_i = 0, myslot_i = 0;
+    uint64_t spare_i = 0;
+    Jobs Ji;
+    Cursor ci;
+    auto setup = [&](uint32_t k) {
+      const uint4 d = lds_read16(&S.desc[k % 3][lane]);
+      const DescView dv = desc_view(P, d, tile_of(k, i), lane);
+      Ji = jobs_setup(dv.abase, dv.span, lane, myslot_i, Ti);
+      cursor_job<true>(ci, Ji, 0, lane);
+      spare_i = spare_line(P, tile_of(k, i), lane);
+      issued_i = 0;
+    };
+    setup(0);
+    // consume side: tile phase kc
+    Jobs Jc = Ji;
+    Cursor cc = ci;
+    uint32_t kc = 0, Tc = Ti, myslot_c = myslot_i, done_c = 0;
+    BodyAcc ba = {0, 0};
+    bool ahead = false;                 // the issue side is in tile kc + 1
+    uint32_t issued = 0, consumed = 0;  // ring pieces, nulls included
+    // Descriptors of tile t are fetched at the end of phase t - 3; a piece
+    // issued after them that has been consumed proves they landed.
+    uint32_t mark_prev = 0, mark_new = 0;
+    if (K > 1) glds<0>(desc_src(P, tile_of(1, i), lane, ntiles), &S.desc[1][0]);
+    if (K > 2) glds<0>(desc_src(P, tile_of(2, i), lane, ntiles), &S.desc[2][0]);
+
+    auto move_on = [&]() {  // the issue side enters tile ti + 1
+      if (ahead || ti + 1 >= K) return;
+      if (consumed <= mark_prev) vm_wait<0>();
+      ++ti;
+      setup(ti);
+      ahead = true;
+    };
+    auto issue_piece = [&](int u) -> bool {  // true: a null piece
+      if (issued_i == Ti) move_on();
+      ++issued;
+      if (issued_i < Ti) {
+        issue_round(ci, Ji, spare_i, &S.ring[u][0], lane);
+        ++issued_i;
+        return false;
+      }
+      glds<OO_RX_BODY_AUX>(spare_i, &S.ring[u][0]);
+      return true;
+    };
+    auto tile_end = [&]() {  // phase kc's tile is consumed
+      SSTAMP(kc, 1);
+      lds_write4(&S.bsum[kc & 1][lane], lane_get(ba.bs, myslot_c));
+      if (!ahead) move_on();
+      if (ahead) {
+        Jc = Ji;
+        cursor_job<false>(cc, Jc, 0, lane);
+        Tc = Ti;
+        myslot_c = myslot_i;
+        ahead = false;
+      } else {
+        Tc = 0;
+      }
+      done_c = 0;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      SSTAMP(kc, 2);
+      block_barrier();
+      SSTAMP(kc, 3);
+      ++kc;
+      if (kc + 2 < K) {
+        glds<0>(desc_src(P, tile_of(kc + 2, i), lane, ntiles), &S.desc[(kc + 2) % 3][0]);
+        mark_prev = mark_new;
+        mark_new = issued;
+      }
+      SSTAMP(kc, 0);
+    };
+
+    SSTAMP(0, 0);
+    // Kept small (one copy of the round and tile-end code): the ring slot is
+    // a register, and a bit per slot marks the null pieces.
+    uint32_t nulls = 0;
+#pragma unroll 1
+    for (int u = 0; u < SR; ++u) nulls |= (uint32_t)issue_piece(u) << u;
+    while (kc < K && done_c == Tc) tile_end();  // empty tiles
+    uint32_t u = 0;
+    while (kc < K) {
+      vm_wait<SR - 2>();  // the two oldest pieces: slots u, u + 1
+      uint4 v[2];
+      lds_read16x2(&S.ring[u][lane], &S.ring[u + 1][lane], v[0], v[1]);
+      consumed += 2;
+#pragma unroll 1
+      for (int j = 0; j < 2; ++j) {
+        if (!((nulls >> (u + j)) & 1u)) {
+          consume_round(cc, Jc, j ? v[1] : v[0], ba, lane);
+          ++done_c;
+          while (kc < K && done_c == Tc) tile_end();
+        }
+      }
+#pragma unroll 1
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t bit = 1u << (u + j);
+        nulls = issue_piece((int)(u + j)) ? (nulls | bit) : (nulls & ~bit);
+      }
+      u = u + 2 == (uint32_t)SR ? 0u : u + 2;
+    }
+    vm_wait<0>();
+    block_barrier();  // the parser's last phase
+  } else {
+    // ---------------- parser
+    Parsed ps[WS];
+    for (uint32_t k = 0; k <= K; ++k) {
+      SSTAMP(k, 0);
+      if (k > 0) {
+#pragma unroll
+        for (int i = 0; i < WS; ++i) {
+          const uint32_t t = tile_of(k - 1, (uint32_t)i);
+          if (t < ntiles) {
+            finish(ps[i], L.s[i].bsum[(k - 1) & 1][lane]);
+            const uint32_t idx = t * P.tile + lane;
+            const bool valid = lane < P.tile && idx < P.n;
+            count_reasons(P, valid, ps[i].r.reason);
+            if (valid) store_record(P, idx, ps[i].r);
+          }
+        }
+      }
+      SSTAMP(k, 1);
+      if (k < K) {
+#pragma unroll
+        for (int i = 0; i < WS; ++i) {
+          const uint32_t t = tile_of(k, (uint32_t)i);
+          if (t < ntiles) ps[i] = parse_tile(P, L.hdr, t, lane);
+        }
+      }
+      SSTAMP(k, 2);
+      block_barrier();
+      SSTAMP(k, 3);
+    }
+  }
 }
 
 }  // namespace oo_rx
 
-// Resident blocks per CU (sizes the persistent grid).
-extern "C" int oo_rx_blocks_per_cu(void) {
+// Resident blocks per CU (sizes the persistent grids).
+extern "C" int oo_rx_blocks_per_cu(int split) {
   int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_kernel, oo_rx::WAVES * 64, 0) !=
-      hipSuccess)
-    return 0;
-  return b;
+  const hipError_t e =
+      split ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_split, (oo_rx::WS + 1) * 64, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_kernel, oo_rx::WAVES * 64, 0);
+  return e == hipSuccess ? b : 0;
 }
 
-extern "C" int oo_rx_waves_per_block(void) { return oo_rx::WAVES; }
+// Tile-processing waves per block: rx_kernel's waves, rx_split's streamers.
+extern "C" int oo_rx_waves_per_block(int split) { return split ? oo_rx::WS : oo_rx::WAVES; }
 
 // Launch one batch on `stream`.
-extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int split, int grid, hipStream_t stream) {
+  if (split)
+    hipLaunchKernelGGL(oo_rx::rx_split, dim3(grid), dim3((oo_rx::WS + 1) * 64), 0, stream, *P);
+  else
+    hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
