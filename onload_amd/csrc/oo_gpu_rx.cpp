@@ -121,6 +121,7 @@ struct oo_gpu_rx_ctx {
   uint32_t* d_occ4 = nullptr;
   Slot6* d_slot6 = nullptr;
   uint32_t* d_occ6 = nullptr;
+  uint8_t* d_zero = nullptr;  // oo_rx::ZERO_LINES x 16 B of zeros
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t grid_split = 1024;  // resident blocks of rx_split
   uint32_t split_min = 512;    // mean bytes per frame from which rx_split runs
@@ -293,6 +294,7 @@ void free_dev(oo_gpu_rx_ctx* c) {
   if (c->d_occ4) (void)hipFree(c->d_occ4);
   if (c->d_slot6) (void)hipFree(c->d_slot6);
   if (c->d_occ6) (void)hipFree(c->d_occ6);
+  if (c->d_zero) (void)hipFree(c->d_zero);
   if (c->d_stage_frames) (void)hipFree(c->d_stage_frames);
   if (c->d_stage_desc) (void)hipFree(c->d_stage_desc);
   if (c->d_stage_out) (void)hipFree(c->d_stage_out);
@@ -463,7 +465,9 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
             hipMalloc(&c->d_slot4, sizeof(Slot4) * c->slot4.size()) == hipSuccess &&
             hipMalloc(&c->d_occ4, sizeof(uint32_t) * c->occ4.size()) == hipSuccess &&
             hipMalloc(&c->d_slot6, sizeof(Slot6) * c->slot6.size()) == hipSuccess &&
-            hipMalloc(&c->d_occ6, sizeof(uint32_t) * c->occ6.size()) == hipSuccess;
+            hipMalloc(&c->d_occ6, sizeof(uint32_t) * c->occ6.size()) == hipSuccess &&
+            hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES) == hipSuccess &&
+            hipMemset(c->d_zero, 0, 16u * oo_rx::ZERO_LINES) == hipSuccess;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
     c->stage_pkts = cfg->host_stage_pkts;
@@ -583,6 +587,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.occ4 = c->d_occ4;
   P.slot6 = c->d_slot6;
   P.occ6 = c->d_occ6;
+  P.zero = c->d_zero;
   P.stamps = c->stamps;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
   // rx_split (parser + streamer waves) for large frames, rx_kernel otherwise;

@@ -66,6 +66,10 @@ struct Slot6 {
 };
 static_assert(sizeof(Slot6) == 64, "v6 slot record layout");
 
+// The zero region read by lanes that have no chunk to load (64 KiB, so
+// those reads spread over the L2 channels).
+constexpr uint32_t ZERO_LINES = 4096;
+
 // Kernel arguments (passed by value).
 struct KParams {
   const uint8_t* frames;
@@ -81,6 +85,7 @@ struct KParams {
   const uint32_t* occ4;  // bit i set: IPv4 slot i is not EMPTY
   const Slot6* slot6;
   const uint32_t* occ6;  // bit i set: IPv6 slot i is not EMPTY
+  const uint8_t* zero;   // ZERO_LINES x 16 B of zeros (lanes with nothing to read)
   uint64_t* stamps;      // diagnostic builds (OO_RX_STAMPS) only; may be null
   uint8_t hwport[OO_GPU_RX_MAX_INTF];
 };

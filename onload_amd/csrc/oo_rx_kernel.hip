@@ -65,13 +65,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define OO_RX_WAVES 2  // rx_kernel: waves per block
 #endif
 #ifndef OO_RX_RING
-#define OO_RX_RING 6  // rx_kernel: body ring slots per wave (even)
+#define OO_RX_RING 4  // rx_kernel: body ring slots per wave (even)
 #endif
 #ifndef OO_RX_WS
 #define OO_RX_WS 2  // rx_split: streamer waves per block (plus one parser)
 #endif
 #ifndef OO_RX_SRING
-#define OO_RX_SRING 8  // rx_split: body ring slots per streamer
+#define OO_RX_SRING 6  // rx_split: body ring slots per streamer (even)
 #endif
 
 constexpr int WAVES = OO_RX_WAVES;
@@ -237,6 +237,15 @@ __device__ __forceinline__ uint32_t group_sum8(uint32_t v) {
   return v;
 }
 
+// The body stream of the frame (see "Body streaming engine") whose window starts at abase (span window bytes):
+// off0 = a0 - abase, in (0, HB], a multiple of 16, and its whole chunks.
+__device__ __forceinline__ uint32_t body_off0(uint64_t abase) {
+  return (uint32_t)(((abase + HB) & ~(uint64_t)127) - abase);
+}
+__device__ __forceinline__ uint32_t body_chunks(uint32_t off0, int span) {
+  return span > HB ? (((uint32_t)span & ~15u) - off0) >> 4 : 0u;
+}
+
 // ---------------------------------------------------------------------------
 // Demux: one lookup stage walked to its end (every match counted).
 
@@ -362,12 +371,26 @@ __device__ __noinline__ uint32_t window_sum_global(uint64_t abase, int S, int E)
   return s;
 }
 
-// handle_rx_csum_bad + handle_rx_pkt + the lookup stages for the packet whose
-// window starts at `my` (16-B cells, rows RB bytes apart; window byte w of
-// the frame's 16-B-aligned start is my[(w >> 4) * RB + (w & 15)]).
+// What the header stage hands the record/demux stage (both parse paths).
+struct Hdr {
+  uint32_t reason;  // PENDING: the checksums passed (or the L4 verdict waits for the body)
+  uint32_t late;    // PENDING, or why a packet that passed them is dropped (IPv4 only)
+  uint32_t flags;   // OO_RX_F_VLAN / OO_RX_F_IP6
+  uint32_t vlan, proto, ip_paylen, l4;
+  bool l3ok, is6, longl4;
+  uint32_t sport, dport;  // network order in host integers
+  uint32_t sa[4], da[4];  // IPv6 addresses, or the IPv4 ones in [0]
+  uint32_t s4, pseudo;
+  int E4;
+};
+
+// The general header walk (any VLAN / IP version / IHL / options / alignment)
+// over the staged window: handle_rx_csum_bad (netif_event.c:1024-1127) and
+// the IPv4 checks of handle_rx_pkt (:293-303, tcp_rx.c:4696-4699).  The
+// window starts at `my` (16-B cells, rows RB bytes apart; window byte w of the
+// frame's 16-B-aligned start is my[(w >> 4) * RB + (w & 15)]).
 template <int RB>
-__device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* my, int shift,
-                                               int len, int intf_i, uint64_t abase, int span) {
+__device__ __forceinline__ Hdr parse_general(const uint8_t* my, int shift, int len, int off0) {
   // Header byte j (j >= 0); bytes at or beyond the frame length read 0.
   auto B = [&](int j) -> uint32_t {
     int w = shift + j;
@@ -379,12 +402,15 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
   auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
   auto N32 = [&](int j) -> uint32_t { return N16(j) | (N16(j + 2) << 16); };
 
-  uint8_t flags = 0;
-  int pre_l3 = 14, vlan = 0;
+  Hdr h;
+  h.flags = 0;
+  h.late = PENDING;
+  int pre_l3 = 14;
+  h.vlan = 0;
   if (BE16(12) == 0x8100u) {  // ci_parse_rx_vlan (netif_event.c:116-132)
     pre_l3 = 18;
-    vlan = (int)(BE16(14) & 0xfffu);
-    flags |= OO_RX_F_VLAN;
+    h.vlan = BE16(14) & 0xfffu;
+    h.flags |= OO_RX_F_VLAN;
   }
   const int l3 = pre_l3;
   uint32_t reason = PENDING;
@@ -406,7 +432,7 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
     } else if (et == 0x86ddu) {  // :1060-1076
       l3ok = true;
       is6 = true;
-      flags |= OO_RX_F_IP6;
+      h.flags |= OO_RX_F_IP6;
       ip_paylen = (int)BE16(l3 + 4);
       proto = B(l3 + 6);
       if (ip_paylen <= 0 || len < pre_l3 + 40 + ip_paylen) reason = OO_RX_R_IP6_LEN;
@@ -454,19 +480,24 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
     }
   }
 
-  // Sums over the staged window: IPv4 header [S3,E3), L4 head [S4,min(E4,HB)).
+  // Sums over the staged window: IPv4 header [S3,E3); the L4 region's
+  // window part: [S4,E4) when it ends inside the window, else [S4,off0)
+  // (signed: the body stream starts at window byte off0, which may lie
+  // before S4).
   const bool need_ip = reason == PENDING && !is6;
   const int S3 = shift + l3, E3 = need_ip ? shift + l3 + ihl4 : S3;
   const int S4 = shift + l4, E4 = need_l4 ? shift + l4 + l4_len : S4;
-  const int E4h = E4 < HB ? E4 : HB;
+  const int cut = E4 > HB ? off0 : E4;
+  const int lo4 = min(S4, cut), hi4 = max(S4, cut);
   uint32_t s3 = 0, s4 = 0;
   if (need_ip || need_l4) {
 #pragma unroll
     for (int k = 0; k < HC; ++k) {
       const uint4 v = *reinterpret_cast<const uint4*>(my + k * RB);
       if (k * 16 < E3) s3 += chunk_sum(v, k * 16, S3, E3);
-      if (k * 16 < E4h) s4 += chunk_sum(v, k * 16, S4, E4h);
+      if (k * 16 < hi4) s4 += chunk_sum(v, k * 16, lo4, hi4);
     }
+    if (cut < S4) s4 = 0u - s4;
   }
   if (reason == PENDING && need_ip) {
     // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
@@ -475,7 +506,7 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
   if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
 
   // L4 verdict now when the region ends inside the window; otherwise it
-  // waits for the body stream (step 5) and the record below is speculative.
+  // waits for the body stream and the record is speculative.
   const bool longl4 = reason == PENDING && need_l4 && E4 > HB;
   if (reason == PENDING && need_l4 && !longl4) {
     uint32_t f = fold16(s4);
@@ -484,36 +515,35 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
       reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
   }
 
-  // ---- handle_rx_pkt, demux, record (per lane; netif_event.c:250-451).
-  oo_gpu_rx_result r;
-  r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
-  r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
-  r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
-  if (l3ok) {
-    r.proto = (uint8_t)proto;
-    r.ip_paylen = (uint16_t)ip_paylen;
-  }
+  h.reason = reason;
+  h.proto = proto;
+  h.ip_paylen = (uint32_t)ip_paylen;
+  h.l4 = (uint32_t)l4;
+  h.l3ok = l3ok;
+  h.is6 = is6;
+  h.longl4 = longl4;
+  h.s4 = s4;
+  h.pseudo = pseudo;
+  h.E4 = E4;
+  h.sport = h.dport = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h.sa[i] = h.da[i] = 0;
   if (reason == PENDING) {
-    flags |= OO_RX_F_CSUM_OK;
-    r.l4_off = (uint16_t)l4;
-    const uint32_t sport = N16(l4), dport = N16(l4 + 2);
-    r.sport_be = (uint16_t)sport;
-    r.dport_be = (uint16_t)dport;
-    uint32_t a6s[4], a6d[4];
+    h.sport = N16(l4);
+    h.dport = N16(l4 + 2);
     if (is6) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        a6s[i] = N32(l3 + 8 + 4 * i);
-        a6d[i] = N32(l3 + 24 + 4 * i);
+        h.sa[i] = N32(l3 + 8 + 4 * i);
+        h.da[i] = N32(l3 + 24 + 4 * i);
       }
-      r.saddr_be = a6s[0] ^ a6s[1] ^ a6s[2] ^ a6s[3];
-      r.daddr_be = a6d[0] ^ a6d[1] ^ a6d[2] ^ a6d[3];
     } else {
-      r.saddr_be = N32(l3 + 12);
-      r.daddr_be = N32(l3 + 16);
+      h.sa[0] = N32(l3 + 12);
+      h.da[0] = N32(l3 + 16);
       const uint32_t frag = BE16(l3 + 6);
+      uint32_t late = PENDING;
       if ((frag & 0x3fffu) != 0 || ip_len > len - pre_l3) {
-        reason = OO_RX_R_IP4_FRAG;  // :293-295
+        late = OO_RX_R_IP4_FRAG;  // netif_event.c:293-295
       } else if (ihl4 > 20) {
         // ci_ip_options_parse (netif_event.c:135-185), signed-char lengths.
         int o = l3 + 20;
@@ -531,11 +561,149 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
             err = true;
           }
         }
-        if (err) reason = OO_RX_R_IP4_OPTS_BAD;
+        if (err) late = OO_RX_R_IP4_OPTS_BAD;
       }
-      if (reason == PENDING && proto == 6u && frag != 0x4000u && frag != 0u)
-        reason = OO_RX_R_TCP_SCATTERED;  // tcp_rx.c:4696-4699
+      if (late == PENDING && proto == 6u && frag != 0x4000u && frag != 0u)
+        late = OO_RX_R_TCP_SCATTERED;  // tcp_rx.c:4696-4699
+      h.late = late;
     }
+  }
+  return h;
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); }
+
+// The fixed-format header (the common frame): 16-B-aligned start, untagged
+// Ethernet, IPv4 with IHL 5, not fragmented, TCP or UDP whose length fields
+// pass the gates.  Every field sits at a fixed window offset, so it comes out
+// of the eight staged cells c[] (window bytes 16k..16k+15 in c[k]) with
+// shifts; the same decisions as parse_general for these frames.  Returns
+// false (h untouched beyond scratch) for every other frame.
+__device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int len, int off0,
+                                            Hdr& h) {
+  const uint32_t ip_len = bswap16(c[1].x);
+  const uint32_t frag = bswap16(c[1].y);
+  const uint32_t proto = c[1].y >> 24;
+  const int ip_paylen = (int)ip_len - 20;
+  const uint32_t udp_len = bswap16(c[2].y >> 16);
+  const int hlen = (int)(((c[2].w >> 16) & 0xf0u) >> 2);
+  bool ok = shift == 0 && off0 >= 48 && len >= 48 && (c[0].w & 0x000fffffu) == 0x00050008u &&
+            ip_paylen > 0 && len >= 14 + (int)ip_len && (frag & 0x3fffu) == 0u;
+  const bool tcp = proto == 6u;
+  ok = ok && (tcp ? (ip_paylen >= 20 && hlen >= 20 && ip_paylen >= hlen)
+                  : (proto == 17u && ip_paylen >= 8 && udp_len >= 8u && udp_len <= (uint32_t)ip_paylen));
+  if (!ok) return false;
+  const uint32_t ucs = c[2].z & 0xffffu;  // UDP checksum field (0: none, IPv4)
+  const bool need_l4 = tcp || ucs != 0u;
+  const int l4_len = tcp ? ip_paylen : (int)udp_len;
+  const int E4 = 34 + l4_len;
+  // IPv4 header words: window bytes [14, 34).
+  const uint32_t s3 = chunk_sum_all(c[1], (c[0].w >> 16) + (c[2].x & 0xffffu));
+  uint32_t reason = fold16(s3) != 0xffffu ? OO_RX_R_IP4_CSUM : PENDING;
+  // Pseudo header (checksum.c:215-223) and the L4 words in the window [34, E4h).
+  const uint32_t pseudo = (c[1].z >> 16) + (c[1].w & 0xffffu) + (c[1].w >> 16) + (c[2].x & 0xffffu) +
+                          (tcp ? 0x0600u + bswap16((uint32_t)ip_paylen) : 0x1100u + (c[2].y >> 16));
+  const int E4h = E4 > HB ? off0 : E4;  // the body stream covers [off0, ...)
+  uint32_t s4 = 0;
+  if (__ballot((E4h & 15) != 0) == 0) {  // the region ends on a cell edge (wave-uniform test)
+#pragma unroll
+    for (int k = 2; k < HC; ++k) {
+      const uint32_t t = chunk_sum_all(c[k], 0u);
+      s4 += E4h >= 16 * k + 16 ? t : 0u;
+    }
+    s4 -= E4h >= 48 ? (c[2].x & 0xffffu) : 0u;  // bytes 32-33: the IPv4 header's
+  } else {
+#pragma unroll
+    for (int k = 2; k < HC; ++k)
+      if (16 * k < E4h) s4 += chunk_sum(c[k], 16 * k, 34, E4h);
+  }
+  const bool longl4 = reason == PENDING && need_l4 && E4 > HB;
+  if (reason == PENDING && need_l4 && !longl4 && fold16(fold16(s4) + pseudo) != 0xffffu)
+    reason = tcp ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+  h.reason = reason;
+  h.late = (tcp && frag != 0x4000u && frag != 0u) ? OO_RX_R_TCP_SCATTERED : PENDING;
+  h.flags = 0;
+  h.vlan = 0;
+  h.proto = proto;
+  h.ip_paylen = (uint32_t)ip_paylen;
+  h.l4 = 34;
+  h.l3ok = true;
+  h.is6 = false;
+  h.longl4 = longl4;
+  h.sport = c[2].x >> 16;
+  h.dport = c[2].y & 0xffffu;
+  h.sa[0] = (c[1].z >> 16) | (c[1].w << 16);
+  h.da[0] = (c[1].w >> 16) | (c[2].x << 16);
+#pragma unroll
+  for (int i = 1; i < 4; ++i) h.sa[i] = h.da[i] = 0;
+  h.s4 = s4;
+  h.pseudo = need_l4 ? pseudo : 0u;
+  h.E4 = need_l4 ? E4 : 34;
+  return true;
+}
+
+// The staged window of this lane's packet in registers (one LDS wait).
+template <int RB>
+__device__ __forceinline__ void read_cells(const uint8_t* my, uint4 (&c)[HC]) {
+  static_assert(HC == 8, "eight window cells");
+  const uint32_t a = (uint32_t)(uintptr_t)(lptr)(my);
+  asm volatile(
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:%9\n\t"
+      "ds_read_b128 %2, %8 offset:%10\n\tds_read_b128 %3, %8 offset:%11\n\t"
+      "ds_read_b128 %4, %8 offset:%12\n\tds_read_b128 %5, %8 offset:%13\n\t"
+      "ds_read_b128 %6, %8 offset:%14\n\tds_read_b128 %7, %8 offset:%15\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3]), "=&v"(c[4]), "=&v"(c[5]),
+        "=&v"(c[6]), "=&v"(c[7])
+      : "v"(a), "n"(RB), "n"(2 * RB), "n"(3 * RB), "n"(4 * RB), "n"(5 * RB), "n"(6 * RB),
+        "n"(7 * RB)
+      : "memory");
+}
+
+// handle_rx_pkt + the lookup stages (netif_event.c:250-451) for one packet
+// (one lane), from its header fields.
+template <int RB>
+__device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* my, int shift,
+                                               int len, int intf_i, uint64_t abase, int span) {
+  const int off0 = (int)body_off0(abase);
+  Hdr h;
+  bool fixed;
+  {
+    uint4 c[HC];
+    read_cells<RB>(my, c);
+    fixed = parse_fixed(c, shift, len, off0, h);
+  }
+  if (__ballot(!fixed) != 0) {
+    if (!fixed) h = parse_general<RB>(my, shift, len, off0);
+  }
+  const int vlan = (int)h.vlan;
+  const uint32_t proto = h.proto;
+  uint32_t reason = h.reason;
+  uint32_t flags = h.flags;
+  const bool is6 = h.is6;
+
+  oo_gpu_rx_result r;
+  r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
+  r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
+  r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+  if (h.l3ok) {
+    r.proto = (uint8_t)proto;
+    r.ip_paylen = (uint16_t)h.ip_paylen;
+  }
+  if (reason == PENDING) {
+    flags |= OO_RX_F_CSUM_OK;
+    r.l4_off = (uint16_t)h.l4;
+    const uint32_t sport = h.sport, dport = h.dport;
+    r.sport_be = (uint16_t)sport;
+    r.dport_be = (uint16_t)dport;
+    if (is6) {
+      r.saddr_be = h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3];
+      r.daddr_be = h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3];
+    } else {
+      r.saddr_be = h.sa[0];
+      r.daddr_be = h.da[0];
+    }
+    reason = h.late;
 
     if (reason == PENDING) {
       // Demux stages in reference order (udp_rx.c:271-306,
@@ -544,8 +712,9 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
       r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
       if (proto == 17u) {
         // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
-        // of the L3 header (udp_rx.c:157-159): bytes 16..19.
-        const uint32_t dd = N32(l3 + 16);
+        // of the L3 header (udp_rx.c:157-159): bytes 16..19, which for
+        // IPv6 are source-address bytes 8..11.
+        const uint32_t dd = is6 ? h.sa[2] : h.da[0];
         if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
       }
       const int nst = proto == 6u ? 3 : 2;
@@ -573,10 +742,10 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
         if (o0) s0 = load_slot6(P, h1_0);
         if (o1) s1 = load_slot6(P, h1_1);
         if (o2) s2 = load_slot6(P, h1_2);
-        m = walk6(P, a6d, dport, a6s, false, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
+        m = walk6(P, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
         stage = 1;
         if (m.n == 0) {
-          m = walk6(P, a6d, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
+          m = walk6(P, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
           stage = 2;
         }
         if (m.n == 0 && nst == 3) {
@@ -623,15 +792,27 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
     }
   }
   r.reason = (uint8_t)reason;
-  r.flags = flags;
+  r.flags = (uint8_t)flags;
   Parsed ps;
   ps.r = r;
-  ps.s4 = s4;
-  ps.pseudo = pseudo;
-  // The body sum covers window bytes [HB, span); an L4 region that ends
-  // before the frame does leaves its complement to subtract.
-  if (longl4 && E4 < span) ps.s4 -= window_sum_global(abase, E4, span);
-  ps.odd_long = (uint32_t)(shift & 1) | (longl4 ? 2u : 0u);
+  ps.s4 = h.s4;
+  ps.pseudo = h.pseudo;
+  // The body stream covers the whole chunks of window bytes [off0, span);
+  // the frame's last partial chunk (staged in cell HC) is summed here, and
+  // an L4 region that ends before the frame does leaves its complement to
+  // subtract.
+  if (h.longl4) {
+    if (span & 15) {
+      uint4 t;
+      asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                   : "=v"(t)
+                   : "v"((uint32_t)(uintptr_t)(lptr)(my)), "n"(HC * RB)
+                   : "memory");
+      ps.s4 += chunk_sum(t, span & ~15, span & ~15, span);
+    }
+    if (h.E4 < span) ps.s4 -= window_sum_global(abase, h.E4, span);
+  }
+  ps.odd_long = (uint32_t)(shift & 1) | (h.longl4 ? 2u : 0u);
   return ps;
 }
 
@@ -662,120 +843,157 @@ __device__ __forceinline__ void store_record(const KParams& P, uint32_t idx,
 // ---------------------------------------------------------------------------
 // Body streaming engine.
 //
-// The packets of a tile with bytes past the window are list positions
-// q = 0..M-1 (lane order); 8-lane group g streams q = g, g+8, ... one after
-// the other, 8 x 16 B = 128 contiguous bytes per round, so one 1-KiB piece
-// (one LDS-DMA instruction) is one round of all eight groups.  Lane (g, j)
-// holds the job at q = g + 8 j, so a group's next job is one cross-lane read
-// away.  Two cursors walk the same schedule: the issue cursor (a ring ahead,
-// with addresses) and the consume cursor; each is a few countdowns per
-// lane, so a round costs a handful of VALU ops on either side.  Each lane
-// sums its chunk (the frame's last chunk masked at the frame end) into a
-// running sum; a group's last round of a job folds the eight lanes and
-// leaves the total with lane (g, job number), where the packet's own lane
-// collects it.
+// A frame's body is its whole 16-B chunks from a0, the 128-B line holding
+// window byte HB, up to the frame end rounded down to 16 B.  The parse covers
+// the rest of the L4 region: the window bytes before a0, and the frame's last
+// partial chunk, which is staged with the header window (cell HC).
+//
+// The tile's frames with a body are its jobs.  Job q goes to lane (g, j) =
+// (q & 7, q >> 3); 8-lane group g streams its jobs j = 0, 1, ... one after
+// the other, 8 x 16 B = one 128-B line per round, so one 1-KiB piece (one
+// LDS-DMA instruction) is one round of all eight groups, and every round reads
+// whole lines (a round straddling two lines reads HBM ~20 % slower:
+// tools/ring_probe.hip).  All groups move to the next job slot on the same
+// round: slot j lasts R_j rounds, the most any of its eight jobs needs.  When
+// the tile's frames differ in size they are first ranked by size, so the jobs
+// of a slot are alike.  Lanes past their job's end read zeros, so consuming a
+// round is four dot products and no masking, and the job/slot bookkeeping is
+// scalar.
 
-struct Jobs {       // a tile's jobs; lane (g, j) holds job q = g + 8 j
-  uint32_t lo, hi;  // body base: frame window byte HB
-  uint32_t nb;      // body chunks (0: no job)
-  uint32_t lim;     // frame end in window coordinates (span)
+struct Jobs {       // a tile's jobs: lane (g, j) holds job q = g + 8 j
+  uint32_t lo, hi;  // a0
+  uint32_t nb;      // whole chunks from a0 (0: no job)
+  uint32_t rj;      // R_(lane & 7): rounds of that job slot
+  uint32_t T;       // rounds of the tile
 };
 
-struct Cursor {   // this lane's view of its group's progress
-  uint32_t ik;    // the group's job number
-  uint32_t grem;  // rounds left in the group's job (0: idle)
-  uint32_t lr;    // rounds left in which this lane has a chunk
-  uint32_t nvl;   // valid bytes of this lane's last chunk of the job
-  uint64_t addr;  // this lane's next chunk (issue cursor only)
-};
+__device__ __forceinline__ uint32_t wave_max(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) v = max(v, lane_get(v, lane ^ d));
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
 
-struct BodyAcc {
-  uint32_t acc, bs;  // running sum; the total of job gj of this lane's group
-};
+// Rank of each lane's key among the wave's, largest first, ties in lane
+// order (a stable LSD radix sort on ballots; `bits` wave-uniform).
+__device__ __forceinline__ uint32_t rank_desc(uint32_t key, uint32_t lane, int bits) {
+  uint32_t k = key, id = lane;  // position `lane` holds (k, id)
+  for (int b = 0; b < bits; ++b) {
+    const bool one = (k >> b) & 1u;
+    const uint64_t ones = __ballot(one);
+    const uint32_t n1 = (uint32_t)__popcll(ones);
+    const uint32_t o_below = __builtin_amdgcn_mbcnt_hi(
+        (uint32_t)(ones >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ones, 0u));
+    const uint32_t dst = one ? o_below : n1 + lane - o_below;
+    k = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)k);
+    id = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)id);
+  }
+  return (uint32_t)__builtin_amdgcn_ds_permute((int)(id << 2), (int)lane);  // to lane id: its rank
+}
 
-// The jobs of the tile whose lanes hold (abase, span): T = rounds of the
-// busiest group; myslot = the lane that will hold this lane's body sum.
+// The jobs of the tile whose lanes hold (abase, span); myslot = the lane that
+// will hold this lane's body sum.  All lanes active.
 __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t lane,
-                                           uint32_t& myslot, uint32_t& T) {
-  const int nwin = (span + 15) >> 4;
-  const uint32_t nb = nwin > HC ? (uint32_t)(nwin - HC) : 0u;
+                                           uint32_t& myslot) {
+  const uint32_t off0 = body_off0(abase);
+  const uint32_t nb = body_chunks(off0, span);
+  const uint32_t rounds = (nb + 7u) >> 3;
   const uint64_t bm = __ballot(nb != 0);
-  const uint32_t M = (uint32_t)__popcll(bm);
-  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-  const uint32_t myq = nb != 0 ? below : M + lane - below;  // a permutation of 0..63
+  uint32_t myq;
+  const uint32_t r0 = bm ? (uint32_t)__builtin_amdgcn_readlane((int)rounds, __builtin_ctzll(bm)) : 0u;
+  if (__ballot(nb != 0 && rounds != r0) == 0) {  // all jobs alike: list order
+    const uint32_t M = (uint32_t)__popcll(bm);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+        (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    myq = nb != 0 ? below : M + lane - below;  // a permutation of 0..63
+  } else {
+    myq = rank_desc(rounds, lane, 32 - __builtin_clz(wave_max(rounds, lane)));
+  }
   myslot = (myq & 7u) * 8u + (myq >> 3);
   const uint32_t jp = (uint32_t)__builtin_amdgcn_ds_permute((int)(myslot << 2), (int)lane);
-  const uint64_t bbase = abase + HB;
+  const uint64_t a0 = abase + off0;
   Jobs J;
-  J.lo = lane_get((uint32_t)bbase, jp);
-  J.hi = lane_get((uint32_t)(bbase >> 32), jp);
-  J.nb = lane_get(nb, jp);  // 0 past the list
-  J.lim = lane_get((uint32_t)span, jp);
-  const uint32_t gr = group_sum8((J.nb + 7u) >> 3);
-  T = (uint32_t)__builtin_amdgcn_readlane((int)gr, 0);
-#pragma unroll
-  for (int g = 1; g < 8; ++g) T = max(T, (uint32_t)__builtin_amdgcn_readlane((int)gr, 8 * g));
+  J.lo = lane_get((uint32_t)a0, jp);
+  J.hi = lane_get((uint32_t)(a0 >> 32), jp);
+  J.nb = lane_get(nb, jp);
+  // R_j: the most rounds over lanes 8g + j
+  uint32_t m = (J.nb + 7u) >> 3;
+  m = max(m, lane_get(m, lane ^ 8u));
+  m = max(m, lane_get(m, lane ^ 16u));
+  m = max(m, lane_get(m, lane ^ 32u));
+  J.rj = m;
+  J.T = (uint32_t)__builtin_amdgcn_readlane((int)group_sum8(m), 0);
   return J;
 }
 
-// Point the cursor at job k of its group (k >= 8: done).  All lanes active.
-template <bool ADDR>
-__device__ __forceinline__ void cursor_job(Cursor& c, const Jobs& J, uint32_t k, uint32_t lane) {
-  const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(k, 7u);
-  const uint32_t nbs = lane_get(J.nb, s), lim = lane_get(J.lim, s);
-  const uint32_t nb = k < 8u ? nbs : 0u;
-  c.ik = k;
-  c.grem = (nb + 7u) >> 3;
-  c.lr = nb > gj ? (nb - gj + 7u) >> 3 : 0u;
-  const int last_pos = HB + 16 * (int)(gj + 8u * (c.lr - 1u));  // this lane's last chunk
-  c.nvl = (uint32_t)min(max((int)lim - last_pos, 0), 16);
-  if (ADDR) c.addr = ((uint64_t)lane_get(J.hi, s) << 32 | lane_get(J.lo, s)) + gj * 16u;
+__device__ __forceinline__ uint32_t slot_rounds(const Jobs& J, uint32_t js) {
+  return js < 8u ? (uint32_t)__builtin_amdgcn_readlane((int)J.rj, (int)js) : 0u;
 }
 
-// One round done: count down; groups whose job ended move to their next.
-template <bool ADDR>
-__device__ __forceinline__ void cursor_step(Cursor& c, const Jobs& J, uint32_t lane) {
-  const bool had = c.grem != 0;
-  c.lr -= c.lr != 0 ? 1u : 0u;
-  if (ADDR) c.addr += 128;
-  c.grem -= had ? 1u : 0u;
-  const bool next = had && c.grem == 0;
-  if (__ballot(next) != 0) {
-    Cursor n;
-    cursor_job<ADDR>(n, J, c.ik + 1, lane);
-    if (next) c = n;
-  }
+struct IssueCursor {
+  uint32_t js, rnd, R;  // job slot, round in it, its rounds (wave-uniform)
+  uint32_t lv;          // rounds of the slot in which this lane has a chunk
+  uint64_t a;           // this lane's next chunk
+};
+
+// Point the issue cursor at job slot js (R = 0: past the last).  All lanes
+// active.
+__device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32_t js,
+                                           uint32_t lane) {
+  const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
+  const uint32_t nb = lane_get(J.nb, s);
+  const uint32_t lo = lane_get(J.lo, s), hi = lane_get(J.hi, s);
+  c.js = js;
+  c.rnd = 0;
+  c.R = slot_rounds(J, js);
+  c.lv = (c.R != 0 && nb > gj) ? (nb - gj + 7u) >> 3 : 0u;
+  c.a = ((uint64_t)hi << 32 | lo) + gj * 16u;
 }
 
-// Issues the cursor's round into `slot` (lanes without a chunk read `spare`).
-__device__ __forceinline__ void issue_round(Cursor& c, const Jobs& J, uint64_t spare, void* slot,
-                                            uint32_t lane) {
-  glds<OO_RX_BODY_AUX>(c.lr != 0 ? c.addr : spare, slot);
-  cursor_step<true>(c, J, lane);
+// Issues the cursor's round into `slot` (lanes without a chunk read zeros).
+__device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint64_t zero,
+                                            void* slot, uint32_t lane) {
+  glds<OO_RX_BODY_AUX>(c.rnd < c.lv ? c.a : zero, slot);
+  c.a += 128;
+  if (++c.rnd == c.R) issue_slot(c, J, c.js + 1, lane);
 }
 
-// Consumes the cursor's round from the landed bytes v.
-__device__ __forceinline__ void consume_round(Cursor& c, const Jobs& J, const uint4& v, BodyAcc& a,
+struct ConsumeCursor {
+  uint32_t js, rnd, R;  // wave-uniform
+  uint32_t acc;         // this lane's running sum
+  uint32_t bs;          // the total of job (group, lane & 7); 0 if none
+};
+
+__device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J) {
+  c.js = 0;
+  c.rnd = 0;
+  c.R = slot_rounds(J, 0);
+  c.acc = 0;
+  c.bs = 0;
+}
+
+// Consumes one round from the landed bytes v.
+__device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
                                               uint32_t lane) {
-  const bool live = c.lr != 0;
-  const uint32_t nv = live ? (c.lr == 1u ? c.nvl : 16u) : 0u;
-  uint32_t s;
-  if (__ballot(nv != 16u && nv != 0u) == 0) {  // whole or no chunks only (wave-uniform)
-    s = chunk_sum_all(v, 0u);
-    s = live ? s : 0u;
-  } else {
-    s = nv == 16u ? chunk_sum_all(v, 0u) : (nv != 0u ? chunk_sum(v, 0, 0, (int)nv) : 0u);
+  uint32_t a = dot(v.x, 0x00010001u, c.acc);
+  uint32_t b = dot(v.y, 0x00010001u, 0u);
+  a = dot(v.z, 0x00010001u, a);
+  b = dot(v.w, 0x00010001u, b);
+  c.acc = a + b;
+  if (++c.rnd == c.R) {  // the slot's jobs end: fold each group
+    const uint32_t t = group_sum8(c.acc);
+    if ((lane & 7u) == c.js) c.bs = t;
+    c.acc = 0;
+    ++c.js;
+    c.rnd = 0;
+    c.R = slot_rounds(J, c.js);
   }
-  a.acc += s;
-  if (__ballot(c.grem == 1u) != 0) {  // some group's job ends this round
-    const uint32_t t = group_sum8(a.acc);
-    if (c.grem == 1u) {
-      if ((lane & 7u) == c.ik) a.bs = t;
-      a.acc = 0;
-    }
-  }
-  cursor_step<false>(c, J, lane);
+}
+
+// A tile's zero lines: 1 KiB of the zero region per tile, so the lanes that
+// read zeros are spread over the L2 channels.
+__device__ __forceinline__ uint64_t zero_line(const KParams& P, uint32_t tile, uint32_t lane) {
+  return reinterpret_cast<uint64_t>(P.zero) +
+         (uint64_t)(((tile * 64u + lane) & (ZERO_LINES - 1u)) * 16u);
 }
 
 // ---------------------------------------------------------------------------
@@ -806,16 +1024,6 @@ __device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, 
   return v;
 }
 
-// A lane that has nothing to load still issues its part of an LDS-DMA
-// instruction (so every instruction is issued by the whole wave and the
-// counted waits stay static); it reads this line instead: its own entry of
-// the descriptor array, which the tile has just brought into L2.  (One
-// common dummy line for every wave of the GPU made a hot spot on one L2
-// channel.)
-__device__ __forceinline__ uint64_t spare_line(const KParams& P, uint32_t tile, uint32_t lane) {
-  return reinterpret_cast<uint64_t>(P.desc) + (uint64_t)((tile * P.tile + lane) % P.n) * 16;
-}
-
 __device__ __forceinline__ uint64_t desc_src(const KParams& P, uint32_t tile, uint32_t lane,
                                              uint32_t ntiles) {
   const uint32_t i = tile * P.tile + lane;
@@ -838,12 +1046,25 @@ __device__ __forceinline__ void count_reasons(const KParams& P, bool valid, uint
   }
 }
 
+// Stages this lane's frame for the parse, lane = packet: window chunks
+// 0..HC-1 in rows 0..HC-1 ([chunk][packet] 16-B cells, rows ROWB apart) and
+// the frame's last partial chunk, when it lies past the window, in row HC.
+// Chunks a frame does not have read zeros.
+__device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64]) {
+  const int nwin = (dv.span + 15) >> 4;
+#pragma unroll
+  for (int k = 0; k < HC; ++k)
+    glds<OO_RX_HDR_AUX>(k < nwin ? dv.abase + (uint64_t)k * 16 : zero, &rows[k][0]);
+  const bool tail = dv.span > HB && (dv.span & 15) != 0;
+  glds<OO_RX_HDR_AUX>(tail ? dv.abase + (uint64_t)(dv.span & ~15) : zero, &rows[HC][0]);
+}
+
 // ---------------------------------------------------------------------------
 // rx_kernel: every wave parses and streams its own tiles.
 
 struct WaveLds {
-  uint4 hdr[HC][64];  // header window, [chunk][packet] 16-B cells
-  uint4 ring[R][64];  // body ring: slot = one round of the eight groups
+  uint4 hdr[HC + 1][64];  // header window + last chunk, [chunk][packet] 16-B cells
+  uint4 ring[R][64];      // body ring: slot = one round of the eight groups
   uint4 desc[64];     // the tile's descriptors
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
@@ -879,24 +1100,27 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     const uint4 d = lds_read16(&L.desc[lane]);
     if (tile + stride < ntiles) glds<0>(desc_src(P, tile + stride, lane, ntiles), &L.desc[0]);
     const DescView dv = desc_view(P, d, tile, lane);
-    const uint64_t spare = spare_line(P, tile, lane);
-    const int nwin = (dv.span + 15) >> 4;
+    const uint64_t zero = zero_line(P, tile, lane);
 
     // ---- 2. header window: chunk k of every frame, lane = packet.
-#pragma unroll
-    for (int k = 0; k < HC; ++k)
-      glds<OO_RX_HDR_AUX>(k < nwin ? dv.abase + (uint64_t)k * 16 : spare, &L.hdr[k][0]);
+#ifndef OO_RX_ABL_NOHDR  // ablation builds (timing experiments only; results are wrong)
+    stage_window(dv, zero, L.hdr);
+#endif
 
     // ---- 3. body jobs; the first R rounds land during the parse.
-    uint32_t myslot, T;
-    const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot, T);
-    T = (T + R - 1) / R * R;  // whole ring turns; the padding rounds are idle
-    Cursor ci, cc;
-    cursor_job<true>(ci, J, 0, lane);
-    cc = ci;
+    uint32_t myslot;
+    const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot);
+    uint32_t T = (J.T + R - 1) / R * R;  // whole ring turns; the padding rounds read zeros
+#ifdef OO_RX_ABL_NOBODY
+    T = 0;
+#endif
+    IssueCursor ci;
+    issue_slot(ci, J, 0, lane);
+    ConsumeCursor cc;
+    consume_start(cc, J);
     if (T != 0) {
 #pragma unroll
-      for (int u = 0; u < R; ++u) issue_round(ci, J, spare, &L.ring[u][0], lane);
+      for (int u = 0; u < R; ++u) issue_round(ci, J, zero, &L.ring[u][0], lane);
       vm_wait<R>();  // the header window (and the next descriptors)
     } else {
       vm_wait<0>();
@@ -905,12 +1129,16 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     STAMP(7, T);
 
     // ---- 4. header work (one packet per lane).
+#ifdef OO_RX_ABL_NOPARSE
+    Parsed ps = {};
+    ps.r.reason = (uint8_t)(lds_read16(&L.hdr[0][lane]).x & 7u);
+#else
     Parsed ps = parse_packet<ROWB>(P, reinterpret_cast<const uint8_t*>(&L.hdr[0][lane]), dv.shift,
                                    dv.len, dv.intf_i, dv.abase, dv.span);
+#endif
     STAMP(3, __builtin_amdgcn_s_memrealtime());
 
     // ---- 5. body stream (T is a multiple of R).
-    BodyAcc ba = {0, 0};
     // Two pieces per step: one wait and one LDS round trip per 2 KiB.
     for (uint32_t k0 = 0; k0 < T; k0 += R) {
 #pragma unroll
@@ -921,17 +1149,17 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
         else vm_wait<0>();
         uint4 v0, v1;
         lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
-        consume_round(cc, J, v0, ba, lane);
-        consume_round(cc, J, v1, ba, lane);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
         if (k + R < T) {
-          issue_round(ci, J, spare, &L.ring[u][0], lane);
-          issue_round(ci, J, spare, &L.ring[u + 1][0], lane);
+          issue_round(ci, J, zero, &L.ring[u][0], lane);
+          issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
         }
       }
     }
     STAMP(4, __builtin_amdgcn_s_memrealtime());
 
-    finish(ps, lane_get(ba.bs, myslot));
+    finish(ps, lane_get(cc.bs, myslot));
     count_reasons(P, dv.valid, ps.r.reason);
     if (dv.valid) store_record(P, dv.idx, ps.r);
     STAMP(5, __builtin_amdgcn_s_memrealtime());
@@ -957,7 +1185,7 @@ struct StreamerLds {
 };
 struct SplitLds {
   StreamerLds s[WS];
-  uint4 hdr[HC][64];  // the parser's header window, [chunk][packet]
+  uint4 hdr[HC + 1][64];  // the parser's header window + last chunks, [chunk][packet]
 };
 static_assert(SR >= 2 && SR % 2 == 0, "a streamer consumes its ring two pieces at a time");
 
@@ -972,17 +1200,13 @@ __device__ __forceinline__ void block_barrier() {
 
 // The parser's header work for tile t: the window staged by LDS-DMA (lane
 // = packet, [chunk][packet] cells, as in rx_kernel), then the common parse.
-__device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (&hdr)[HC][64], uint32_t t,
+__device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (*hdr)[64], uint32_t t,
                                              uint32_t lane) {
   const uint32_t idx = t * P.tile + lane;
   uint4 d = make_uint4(0, 0, 0, 0);
   if (lane < P.tile && idx < P.n) d = *reinterpret_cast<const uint4*>(P.desc + idx);
   const DescView dv = desc_view(P, d, t, lane);
-  // LDS-DMA staging, lane = packet, [chunk][packet] cells.
-  const int nwin = (dv.span + 15) >> 4;
-#pragma unroll
-  for (int k = 0; k < HC; ++k)
-    glds<OO_RX_HDR_AUX>(k < nwin ? dv.abase + (uint64_t)k * 16 : spare_line(P, t, lane), &hdr[k][0]);
+  stage_window(dv, zero_line(P, t, lane), hdr);
   vm_wait<0>();
   return parse_packet<ROWB>(P, reinterpret_cast<const uint8_t*>(&hdr[0][lane]), dv.shift, dv.len,
                             dv.intf_i, dv.abase, dv.span);
@@ -1026,23 +1250,24 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
 
     // issue side: tile ti, its jobs and cursor
     uint32_t ti = 0, Ti = 0, issued_i = 0, myslot_i = 0;
-    uint64_t spare_i = 0;
+    uint64_t zero_i = 0;
     Jobs Ji;
-    Cursor ci;
+    IssueCursor ci;
     auto setup = [&](uint32_t k) {
       const uint4 d = lds_read16(&S.desc[k % 3][lane]);
       const DescView dv = desc_view(P, d, tile_of(k, i), lane);
-      Ji = jobs_setup(dv.abase, dv.span, lane, myslot_i, Ti);
-      cursor_job<true>(ci, Ji, 0, lane);
-      spare_i = spare_line(P, tile_of(k, i), lane);
+      Ji = jobs_setup(dv.abase, dv.span, lane, myslot_i);
+      Ti = (Ji.T + 1u) & ~1u;  // whole pairs: a tile starts on an even slot
+      issue_slot(ci, Ji, 0, lane);
+      zero_i = zero_line(P, tile_of(k, i), lane);
       issued_i = 0;
     };
     setup(0);
     // consume side: tile phase kc
     Jobs Jc = Ji;
-    Cursor cc = ci;
+    ConsumeCursor cc;
+    consume_start(cc, Jc);
     uint32_t kc = 0, Tc = Ti, myslot_c = myslot_i, done_c = 0;
-    BodyAcc ba = {0, 0};
     bool ahead = false;                 // the issue side is in tile kc + 1
     uint32_t issued = 0, consumed = 0;  // ring pieces, nulls included
     // Descriptors of tile t are fetched at the end of phase t - 3; a piece
@@ -1058,24 +1283,27 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
       setup(ti);
       ahead = true;
     };
-    auto issue_piece = [&](int u) -> bool {  // true: a null piece
+    // Issues the pair of slots u, u + 1; true: a null pair.
+    auto issue_pair = [&](uint32_t u) -> bool {
       if (issued_i == Ti) move_on();
-      ++issued;
+      issued += 2;
       if (issued_i < Ti) {
-        issue_round(ci, Ji, spare_i, &S.ring[u][0], lane);
-        ++issued_i;
+        issue_round(ci, Ji, zero_i, &S.ring[u][0], lane);
+        issue_round(ci, Ji, zero_i, &S.ring[u + 1][0], lane);
+        issued_i += 2;
         return false;
       }
-      glds<OO_RX_BODY_AUX>(spare_i, &S.ring[u][0]);
+      glds<OO_RX_BODY_AUX>(zero_i, &S.ring[u][0]);
+      glds<OO_RX_BODY_AUX>(zero_i, &S.ring[u + 1][0]);
       return true;
     };
     auto tile_end = [&]() {  // phase kc's tile is consumed
       SSTAMP(kc, 1);
-      lds_write4(&S.bsum[kc & 1][lane], lane_get(ba.bs, myslot_c));
+      lds_write4(&S.bsum[kc & 1][lane], lane_get(cc.bs, myslot_c));
       if (!ahead) move_on();
       if (ahead) {
         Jc = Ji;
-        cursor_job<false>(cc, Jc, 0, lane);
+        consume_start(cc, Jc);
         Tc = Ti;
         myslot_c = myslot_i;
         ahead = false;
@@ -1097,31 +1325,27 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
     };
 
     SSTAMP(0, 0);
-    // Kept small (one copy of the round and tile-end code): the ring slot is
-    // a register, and a bit per slot marks the null pieces.
+    // The ring slot is a register and a bit per slot pair marks the null
+    // pairs (one copy of the round and tile-end code).
     uint32_t nulls = 0;
 #pragma unroll 1
-    for (int u = 0; u < SR; ++u) nulls |= (uint32_t)issue_piece(u) << u;
+    for (uint32_t u = 0; u < (uint32_t)SR; u += 2) nulls |= (uint32_t)issue_pair(u) << (u >> 1);
     while (kc < K && done_c == Tc) tile_end();  // empty tiles
     uint32_t u = 0;
     while (kc < K) {
       vm_wait<SR - 2>();  // the two oldest pieces: slots u, u + 1
-      uint4 v[2];
-      lds_read16x2(&S.ring[u][lane], &S.ring[u + 1][lane], v[0], v[1]);
+      uint4 v0, v1;
+      lds_read16x2(&S.ring[u][lane], &S.ring[u + 1][lane], v0, v1);
       consumed += 2;
-#pragma unroll 1
-      for (int j = 0; j < 2; ++j) {
-        if (!((nulls >> (u + j)) & 1u)) {
-          consume_round(cc, Jc, j ? v[1] : v[0], ba, lane);
-          ++done_c;
-          while (kc < K && done_c == Tc) tile_end();
-        }
+      const uint32_t bit = 1u << (u >> 1);
+      if (!(nulls & bit)) {
+        consume_round(cc, Jc, v0, lane);
+        consume_round(cc, Jc, v1, lane);
+        done_c += 2;
+        while (kc < K && done_c == Tc) tile_end();
       }
-#pragma unroll 1
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t bit = 1u << (u + j);
-        nulls = issue_piece((int)(u + j)) ? (nulls | bit) : (nulls & ~bit);
-      }
+      nulls = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)(issue_pair(u) ? (nulls | bit) : (nulls & ~bit)));
       u = u + 2 == (uint32_t)SR ? 0u : u + 2;
     }
     vm_wait<0>();
@@ -1149,7 +1373,11 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
 #pragma unroll
         for (int i = 0; i < WS; ++i) {
           const uint32_t t = tile_of(k, (uint32_t)i);
+#ifdef OO_RX_ABL_NOPARSE
+          if (t < ntiles) ps[i] = Parsed{};
+#else
           if (t < ntiles) ps[i] = parse_tile(P, L.hdr, t, lane);
+#endif
         }
       }
       SSTAMP(k, 2);

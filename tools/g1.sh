@@ -4,6 +4,5 @@ for k in split lanes; do
   OO_RX_KERNEL=$k timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t_$k.log 2>&1
   rc=$?; tail -4 gpurun_out/t_$k.log; echo "tests $k rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
-for c in 2 3; do
-SWEEP="OO_RX_KERNEL=split OO_RX_KERNEL=lanes" CONFIG=$c STEPS=100 bash tools/sweep.sh || exit $?
-done
+SWEEP="OO_RX_KERNEL=split OO_RX_KERNEL=lanes OO_RX_KERNEL=split;OO_RX_LIB=build/var_noparse.so OO_RX_KERNEL=lanes;OO_RX_LIB=build/var_nohp.so" CONFIG=2 STEPS=100 bash tools/sweep.sh || exit $?
+for c in 3 4 5; do SWEEP="OO_RX_KERNEL=split OO_RX_KERNEL=lanes" CONFIG=$c STEPS=30 bash tools/sweep.sh || exit $?; done

@@ -95,10 +95,14 @@ static void run(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
 // Grouped variant: each wave owns 64-frame tiles of FB-byte frames; groups
 // of G lanes stream one frame each (G*16 contiguous bytes per round), so an
 // instruction touches 64/G frames.
-template <int R, int G>
+template <int R, int G, int FB = 1536, bool AL = false>
 __global__ __launch_bounds__(64) void ring_grp(const u32x4* __restrict__ p, size_t nframes,
                                                uint32_t* out) {
-  constexpr uint32_t fb16 = 96;
+  // frames of FB bytes at FB-byte stride (16-B aligned starts: FB 1536, or
+  // not: 1514, whose 16-B chunk runs straddle 128-B lines)
+  // AL: rounds start on the 128-B line at or below the frame (one more
+  // chunk run per frame; the extra bytes would be masked)
+  constexpr uint32_t fb16 = (FB + 15) / 16 + (AL ? 8 : 0);
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   const int lane = threadIdx.x;
   const int g = lane / G, j = lane % G;
@@ -113,7 +117,8 @@ __global__ __launch_bounds__(64) void ring_grp(const u32x4* __restrict__ p, size
       const uint32_t fi = k / rounds, r = k % rounds;
       const uint32_t c = r * G + j;
       const size_t frame = t * 64 + g + fi * NG;
-      return (k < total && c < fb16) ? p + frame * fb16 + c : p;
+      const size_t b16 = AL ? ((frame * FB) & ~(size_t)127) / 16 : (frame * FB) / 16;
+      return (k < total && c < fb16) ? p + b16 + c : p;
     };
 #pragma unroll
     for (int u = 0; u < R; ++u)
@@ -132,12 +137,12 @@ __global__ __launch_bounds__(64) void ring_grp(const u32x4* __restrict__ p, size
   if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <int R, int G>
+template <int R, int G, int FB = 1536, bool AL = false>
 static void run_grp(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
   const size_t lds = (size_t)R * 1024;
-  const size_t nframes = bytes / 1536 / 64 * 64;
+  const size_t nframes = (bytes - 4096) / FB / 64 * 64;
   int bpc = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, ring_grp<R, G>, 64, lds);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, ring_grp<R, G, FB, AL>, 64, lds);
   for (int m : {4, 8, 12, 16}) {
     if (m > bpc) break;
     const int grid = cu * m;
@@ -147,7 +152,7 @@ static void run_grp(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
     float best = 1e9f;
     for (int r = 0; r < 10; ++r) {
       (void)hipEventRecord(e0, 0);
-      hipLaunchKernelGGL((ring_grp<R, G>), dim3(grid), dim3(64), lds, 0, a, nframes, o);
+      hipLaunchKernelGGL((ring_grp<R, G, FB, AL>), dim3(grid), dim3(64), lds, 0, a, nframes, o);
       (void)hipEventRecord(e1, 0);
       (void)hipEventSynchronize(e1);
       float ms;
@@ -155,8 +160,8 @@ static void run_grp(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
       if (r >= 2 && ms < best) best = ms;
     }
     if (hipGetLastError() != hipSuccess) { printf("launch error\n"); exit(1); }
-    printf("{\"grouped\":%d,\"slots\":%d,\"waves_per_cu\":%d,\"GBps\":%.1f}\n", G, R, m,
-           nframes * 1536 / (best * 1e-3) / 1e9);
+    printf("{\"grouped\":%d,\"aligned_rounds\":%d,\"frame\":%d,\"slots\":%d,\"waves_per_cu\":%d,\"GBps\":%.1f}\n", G, (int)AL, FB,
+           (int)AL, R, m, nframes * FB / (best * 1e-3) / 1e9);
   }
 }
 
@@ -174,11 +179,8 @@ int main(int argc, char** argv) {
     run<16, 1>(a, bytes, o, cu);
     run<32, 1>(a, bytes, o, cu);
   }
-  run_grp<4, 8>(a, bytes, o, cu);
-  run_grp<6, 8>(a, bytes, o, cu);
-  run_grp<4, 16>(a, bytes, o, cu);
-  run_grp<4, 32>(a, bytes, o, cu);
-  run_grp<4, 64>(a, bytes, o, cu);
-  run_grp<8, 64>(a, bytes, o, cu);
+  run_grp<6, 8, 1514>(a, bytes, o, cu);
+  run_grp<6, 8, 1514, true>(a, bytes, o, cu);
+  run_grp<8, 8, 1514, true>(a, bytes, o, cu);
   return 0;
 }
