@@ -466,7 +466,7 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
             hipMalloc(&c->d_occ4, sizeof(uint32_t) * c->occ4.size()) == hipSuccess &&
             hipMalloc(&c->d_slot6, sizeof(Slot6) * c->slot6.size()) == hipSuccess &&
             hipMalloc(&c->d_occ6, sizeof(uint32_t) * c->occ6.size()) == hipSuccess &&
-            hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES) == hipSuccess &&
+            hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + 64u * 32u) == hipSuccess &&
             hipMemset(c->d_zero, 0, 16u * oo_rx::ZERO_LINES) == hipSuccess;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
@@ -588,6 +588,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.slot6 = c->d_slot6;
   P.occ6 = c->d_occ6;
   P.zero = c->d_zero;
+  P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
   P.stamps = c->stamps;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
   // rx_split (parser + streamer waves) for large frames, rx_kernel otherwise;

@@ -86,6 +86,7 @@ struct KParams {
   const Slot6* slot6;
   const uint32_t* occ6;  // bit i set: IPv6 slot i is not EMPTY
   const uint8_t* zero;   // ZERO_LINES x 16 B of zeros (lanes with nothing to read)
+  uint8_t* sink;         // 64 x 32 B written by lanes without a packet (rx_kernel)
   uint64_t* stamps;      // diagnostic builds (OO_RX_STAMPS) only; may be null
   uint8_t hwport[OO_GPU_RX_MAX_INTF];
 };

@@ -384,18 +384,27 @@ struct Hdr {
   int E4;
 };
 
+// A packet's staged window in LDS (stage_window): a 128-B row whose 16-B
+// cell k sits at row + 16 * ((k + rot) & 7), and the frame's last chunk.
+struct Win {
+  const uint8_t* row;
+  uint32_t rot;
+  const uint8_t* tail;
+  __device__ __forceinline__ const uint8_t* cell(int k) const {
+    return row + ((((uint32_t)k + rot) & 7u) << 4);
+  }
+};
+
 // The general header walk (any VLAN / IP version / IHL / options / alignment)
 // over the staged window: handle_rx_csum_bad (netif_event.c:1024-1127) and
-// the IPv4 checks of handle_rx_pkt (:293-303, tcp_rx.c:4696-4699).  The
-// window starts at `my` (16-B cells, rows RB bytes apart; window byte w of the
-// frame's 16-B-aligned start is my[(w >> 4) * RB + (w & 15)]).
-template <int RB>
-__device__ __forceinline__ Hdr parse_general(const uint8_t* my, int shift, int len, int off0) {
+// the IPv4 checks of handle_rx_pkt (:293-303, tcp_rx.c:4696-4699).  Window
+// byte w is the frame's 16-B-aligned start + w.
+__device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, int off0) {
   // Header byte j (j >= 0); bytes at or beyond the frame length read 0.
   auto B = [&](int j) -> uint32_t {
     int w = shift + j;
     w = w < HB ? w : HB - 1;
-    const uint32_t v = my[(w >> 4) * RB + (w & 15)];
+    const uint32_t v = W.cell(w >> 4)[w & 15];
     return j < len ? v : 0u;
   };
   auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
@@ -493,7 +502,7 @@ __device__ __forceinline__ Hdr parse_general(const uint8_t* my, int shift, int l
   if (need_ip || need_l4) {
 #pragma unroll
     for (int k = 0; k < HC; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4*>(my + k * RB);
+      const uint4 v = *reinterpret_cast<const uint4*>(W.cell(k));
       if (k * 16 < E3) s3 += chunk_sum(v, k * 16, S3, E3);
       if (k * 16 < hi4) s4 += chunk_sum(v, k * 16, lo4, hi4);
     }
@@ -643,38 +652,37 @@ __device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int
 }
 
 // The staged window of this lane's packet in registers (one LDS wait).
-template <int RB>
-__device__ __forceinline__ void read_cells(const uint8_t* my, uint4 (&c)[HC]) {
+__device__ __forceinline__ void read_cells(const Win& W, uint4 (&c)[HC]) {
   static_assert(HC == 8, "eight window cells");
-  const uint32_t a = (uint32_t)(uintptr_t)(lptr)(my);
+  uint32_t a[HC];
+#pragma unroll
+  for (int k = 0; k < HC; ++k) a[k] = (uint32_t)(uintptr_t)(lptr)(W.cell(k));
   asm volatile(
-      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:%9\n\t"
-      "ds_read_b128 %2, %8 offset:%10\n\tds_read_b128 %3, %8 offset:%11\n\t"
-      "ds_read_b128 %4, %8 offset:%12\n\tds_read_b128 %5, %8 offset:%13\n\t"
-      "ds_read_b128 %6, %8 offset:%14\n\tds_read_b128 %7, %8 offset:%15\n\t"
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\t"
+      "ds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\t"
+      "ds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\t"
+      "ds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\t"
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3]), "=&v"(c[4]), "=&v"(c[5]),
         "=&v"(c[6]), "=&v"(c[7])
-      : "v"(a), "n"(RB), "n"(2 * RB), "n"(3 * RB), "n"(4 * RB), "n"(5 * RB), "n"(6 * RB),
-        "n"(7 * RB)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
       : "memory");
 }
 
 // handle_rx_pkt + the lookup stages (netif_event.c:250-451) for one packet
 // (one lane), from its header fields.
-template <int RB>
-__device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* my, int shift,
+__device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, int shift,
                                                int len, int intf_i, uint64_t abase, int span) {
   const int off0 = (int)body_off0(abase);
   Hdr h;
   bool fixed;
   {
     uint4 c[HC];
-    read_cells<RB>(my, c);
+    read_cells(W, c);
     fixed = parse_fixed(c, shift, len, off0, h);
   }
   if (__ballot(!fixed) != 0) {
-    if (!fixed) h = parse_general<RB>(my, shift, len, off0);
+    if (!fixed) h = parse_general(W, shift, len, off0);
   }
   const int vlan = (int)h.vlan;
   const uint32_t proto = h.proto;
@@ -721,8 +729,10 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
       Match m = {-1, 0};
       int stage = 0;
       // Every stage's first slot bit, its successor's bit and the first
-      // slot's record are loaded up front (two dependent levels); the walks
-      // then usually need nothing more.
+      // slot's record are loaded up front (two dependent levels; loading the
+      // records unconditionally, one level, was slower: the 2-MiB record
+      // array does not stay in L2 beside the stream); the walks then
+      // usually need nothing more.
       if (is6) {
         const uint32_t zero[4] = {0, 0, 0, 0};
         const uint32_t dx = r.daddr_be, sx = r.saddr_be;
@@ -806,7 +816,7 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const uint8_t* 
       uint4 t;
       asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
                    : "=v"(t)
-                   : "v"((uint32_t)(uintptr_t)(lptr)(my)), "n"(HC * RB)
+                   : "v"((uint32_t)(uintptr_t)(lptr)(W.tail)), "n"(0)
                    : "memory");
       ps.s4 += chunk_sum(t, span & ~15, span & ~15, span);
     }
@@ -1046,29 +1056,100 @@ __device__ __forceinline__ void count_reasons(const KParams& P, bool valid, uint
   }
 }
 
-// Stages this lane's frame for the parse, lane = packet: window chunks
-// 0..HC-1 in rows 0..HC-1 ([chunk][packet] 16-B cells, rows ROWB apart) and
-// the frame's last partial chunk, when it lies past the window, in row HC.
-// Chunks a frame does not have read zeros.
-__device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64]) {
-  const int nwin = (dv.span + 15) >> 4;
+// Stages the tile's header windows for the parse.  Rows 0..HC-1 hold the
+// windows packet-major: packet p's 128-B window is row-major at byte 128 p,
+// its cell k at 16 * ((k - p) & 7) within it, so one LDS-DMA instruction
+// reads eight packets' windows, eight lanes (one 128-B run) per packet --
+// 8-16 cache lines per instruction, not 64 -- and the packet-per-lane reads
+// of any one cell fall in distinct banks.  Row HC holds each frame's last
+// partial chunk when it lies past the window (lane = packet).  Chunks a frame
+// does not have read zeros.  All lanes active.
+__device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64],
+                                             uint32_t lane) {
+  const uint32_t lo = (uint32_t)dv.abase, hi = (uint32_t)(dv.abase >> 32);
 #pragma unroll
-  for (int k = 0; k < HC; ++k)
-    glds<OO_RX_HDR_AUX>(k < nwin ? dv.abase + (uint64_t)k * 16 : zero, &rows[k][0]);
+  for (int i = 0; i < HC; ++i) {
+    const uint32_t p = (uint32_t)i * 8u + (lane >> 3);
+    const uint32_t c = ((lane & 7u) + p) & 7u;
+    const uint64_t ab = (uint64_t)lane_get(hi, p) << 32 | lane_get(lo, p);
+    const int nwin = ((int)lane_get((uint32_t)dv.span, p) + 15) >> 4;
+    glds<OO_RX_HDR_AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
+  }
   const bool tail = dv.span > HB && (dv.span & 15) != 0;
   glds<OO_RX_HDR_AUX>(tail ? dv.abase + (uint64_t)(dv.span & ~15) : zero, &rows[HC][0]);
 }
 
+__device__ __forceinline__ Win window_of(uint4 (*rows)[64], uint32_t lane) {
+  Win W;
+  W.row = reinterpret_cast<const uint8_t*>(&rows[0][0]) + 128u * lane;
+  W.rot = (8u - (lane & 7u)) & 7u;
+  W.tail = reinterpret_cast<const uint8_t*>(&rows[HC][lane]);
+  return W;
+}
+
 // ---------------------------------------------------------------------------
-// rx_kernel: every wave parses and streams its own tiles.
+// rx_kernel: every wave parses and streams its own tiles, software-pipelined:
+// while a tile's body streams, the next tile's header windows (and the
+// descriptors of the tile after it) land in LDS, so each tile starts with its
+// headers in place.  A wave's vector-memory operations (loads, LDS-DMA,
+// stores) retire in issue order, and every wait counts the operations issued
+// after the ones it needs: NHS staging operations per tile (HC + 1 header rows
+// and one descriptor line) and NST record stores, both issued by the whole
+// wave whatever its lanes hold, so the counts are static.
+
+constexpr int NHS = HC + 2;
+constexpr int NST = 2;
 
 struct WaveLds {
-  uint4 hdr[HC + 1][64];  // header window + last chunk, [chunk][packet] 16-B cells
-  uint4 ring[R][64];      // body ring: slot = one round of the eight groups
-  uint4 desc[64];     // the tile's descriptors
+  uint4 hdr[HC + 1][64];        // header windows (stage_window)
+  uint4 ring[R][64];            // body ring: slot = one round of the eight groups
+  uint4 desc[2][64];            // descriptors of this tile and of the next
+  uint32_t cnt[OO_RX_R_COUNT];  // per-reason counts
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
 constexpr int WAVE_U4 = (int)(sizeof(WaveLds) / 16);
+
+__device__ __forceinline__ void lds_write4(void* p, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_add4(void* p, uint32_t v) {
+  asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_read4(const void* p) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(v)
+               : "v"((uint32_t)(uintptr_t)(lptr)(p))
+               : "memory");
+  return v;
+}
+
+// vm_wait with a count that is a constant only after unrolling.
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+#define OO_W(k) \
+  case k:       \
+    vm_wait<k>(); \
+    break;
+    OO_W(0) OO_W(1) OO_W(2) OO_W(3) OO_W(4) OO_W(5) OO_W(6) OO_W(7) OO_W(8) OO_W(9) OO_W(10)
+    OO_W(11) OO_W(12) OO_W(13) OO_W(14) OO_W(15) OO_W(16) OO_W(17) OO_W(18) OO_W(19) OO_W(20)
+    OO_W(21) OO_W(22) OO_W(23) OO_W(24) OO_W(25) OO_W(26) OO_W(27) OO_W(28) OO_W(29) OO_W(30)
+#undef OO_W
+    default:
+      vm_wait<0>();
+  }
+}
+
+// The record of every lane: lanes without a packet write the sink, so the
+// wave always issues exactly NST stores.
+__device__ __forceinline__ void store_records(const KParams& P, bool valid, uint32_t idx,
+                                              const oo_gpu_rx_result& r, uint32_t lane) {
+  uint4* o = valid ? reinterpret_cast<uint4*>(P.out + idx)
+                   : reinterpret_cast<uint4*>(P.sink) + 2u * lane;
+  const uint4* src = reinterpret_cast<const uint4*>(&r);
+  o[0] = src[0];
+  o[1] = src[1];
+}
 
 __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
   // All LDS in one __shared__ array (a second object can make hipcc wait
@@ -1082,32 +1163,29 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
   const uint32_t ntiles = (P.n + P.tile - 1) / P.tile;
   const uint32_t stride = gridDim.x * WAVES;
   uint32_t tile = blockIdx.x * WAVES + wave;
-  // Lanes with nothing to load read this always-mapped line instead, so
-  // every LDS-DMA instruction is issued by the whole wave and the counted
-  // waits stay static.
-  if (tile < ntiles) glds<0>(desc_src(P, tile, lane, ntiles), &L.desc[0]);
-  vm_wait<0>();
+  if (tile >= ntiles) return;
   const uint32_t gwave = blockIdx.x * WAVES + wave;
-  uint32_t it_ = 0;
   (void)gwave;
-  (void)it_;
+  if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
 
-  for (; tile < ntiles; tile += stride, ++it_) {
+  // Prologue: this tile's descriptors, then the next tile's and this tile's
+  // header windows.
+  glds<0>(desc_src(P, tile, lane, ntiles), &L.desc[0][0]);
+  vm_wait<0>();
+  glds<0>(desc_src(P, tile + stride, lane, ntiles), &L.desc[1][0]);
+  {
+    const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), tile, lane);
+    stage_window(d0, zero_line(P, tile, lane), L.hdr, lane);
+  }
+
+  uint32_t b = 0, it_ = 0;
+  for (; tile < ntiles; tile += stride, b ^= 1u, ++it_) {
     STAMP(0, __builtin_amdgcn_s_memrealtime());
     STAMP(6, tile);
-    // ---- 1. descriptors (landed: every earlier wait retired them), then
-    // the next tile's.
-    const uint4 d = lds_read16(&L.desc[lane]);
-    if (tile + stride < ntiles) glds<0>(desc_src(P, tile + stride, lane, ntiles), &L.desc[0]);
-    const DescView dv = desc_view(P, d, tile, lane);
+    const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), tile, lane);
     const uint64_t zero = zero_line(P, tile, lane);
 
-    // ---- 2. header window: chunk k of every frame, lane = packet.
-#ifndef OO_RX_ABL_NOHDR  // ablation builds (timing experiments only; results are wrong)
-    stage_window(dv, zero, L.hdr);
-#endif
-
-    // ---- 3. body jobs; the first R rounds land during the parse.
+    // ---- body jobs; the first R rounds land during the parse.
     uint32_t myslot;
     const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot);
     uint32_t T = (J.T + R - 1) / R * R;  // whole ring turns; the padding rounds read zeros
@@ -1118,40 +1196,55 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     issue_slot(ci, J, 0, lane);
     ConsumeCursor cc;
     consume_start(cc, J);
+    // This tile's header windows: older than the previous tile's NST stores
+    // (none before the first tile) and the R rounds issued here.
     if (T != 0) {
 #pragma unroll
       for (int u = 0; u < R; ++u) issue_round(ci, J, zero, &L.ring[u][0], lane);
-      vm_wait<R>();  // the header window (and the next descriptors)
+      if (it_ == 0) vm_wait<R>();
+      else vm_wait<R + NST>();
     } else {
-      vm_wait<0>();
+      if (it_ == 0) vm_wait<0>();
+      else vm_wait<NST>();
     }
     STAMP(1, __builtin_amdgcn_s_memrealtime());
     STAMP(7, T);
 
-    // ---- 4. header work (one packet per lane).
+    // ---- header work (one packet per lane).
 #ifdef OO_RX_ABL_NOPARSE
     Parsed ps = {};
     ps.r.reason = (uint8_t)(lds_read16(&L.hdr[0][lane]).x & 7u);
 #else
-    Parsed ps = parse_packet<ROWB>(P, reinterpret_cast<const uint8_t*>(&L.hdr[0][lane]), dv.shift,
-                                   dv.len, dv.intf_i, dv.abase, dv.span);
+    Parsed ps = parse_packet(P, window_of(L.hdr, lane), dv.shift, dv.len, dv.intf_i, dv.abase,
+                             dv.span);
 #endif
     STAMP(3, __builtin_amdgcn_s_memrealtime());
 
-    // ---- 5. body stream (T is a multiple of R).
-    // Two pieces per step: one wait and one LDS round trip per 2 KiB.
+    // ---- stage the next tile: descriptors of the tile after it into this
+    // tile's buffer, and its header windows.
+    glds<0>(desc_src(P, tile + 2u * stride, lane, ntiles), &L.desc[b][0]);
+    {
+      const uint32_t nt = tile + stride;
+      const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
+      stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
+    }
+
+    // ---- body stream (T is a multiple of R), two pieces per step.  Pieces
+    // newer than the awaited pair: the rest of the ring, plus the NHS
+    // staging operations in the first turn; none past T.
     for (uint32_t k0 = 0; k0 < T; k0 += R) {
+      const bool first = k0 == 0, last = k0 + R == T;
 #pragma unroll
       for (int u = 0; u < R; u += 2) {
-        const uint32_t k = k0 + (uint32_t)u;
-        // Pieces k+2 .. min(T, k+R)-1 may still be in flight.
-        if (k + R <= T) vm_wait<R - 2>();
-        else vm_wait<0>();
+        if (first && last) vm_wait_n(R - 2 - u + NHS);
+        else if (first) vm_wait_n(R - 2 + NHS);
+        else if (last) vm_wait_n(R - 2 - u);
+        else vm_wait<R - 2>();
         uint4 v0, v1;
         lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
         consume_round(cc, J, v0, lane);
         consume_round(cc, J, v1, lane);
-        if (k + R < T) {
+        if (!last) {
           issue_round(ci, J, zero, &L.ring[u][0], lane);
           issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
         }
@@ -1160,9 +1253,18 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     STAMP(4, __builtin_amdgcn_s_memrealtime());
 
     finish(ps, lane_get(cc.bs, myslot));
-    count_reasons(P, dv.valid, ps.r.reason);
-    if (dv.valid) store_record(P, dv.idx, ps.r);
+    if (P.counters != nullptr && dv.valid) lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
+    store_records(P, dv.valid, dv.idx, ps.r, lane);
     STAMP(5, __builtin_amdgcn_s_memrealtime());
+  }
+
+  // Per-reason counts: one global atomic per reason seen by the wave.
+  if (P.counters != nullptr) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < OO_RX_R_COUNT) {
+      const uint32_t c = lds_read4(&L.cnt[lane]);
+      if (c != 0) atomicAdd(&P.counters[lane], c);
+    }
   }
 }
 
@@ -1189,9 +1291,6 @@ struct SplitLds {
 };
 static_assert(SR >= 2 && SR % 2 == 0, "a streamer consumes its ring two pieces at a time");
 
-__device__ __forceinline__ void lds_write4(void* p, uint32_t v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(v) : "memory");
-}
 __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -1206,9 +1305,9 @@ __device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (*hdr)[64],
   uint4 d = make_uint4(0, 0, 0, 0);
   if (lane < P.tile && idx < P.n) d = *reinterpret_cast<const uint4*>(P.desc + idx);
   const DescView dv = desc_view(P, d, t, lane);
-  stage_window(dv, zero_line(P, t, lane), hdr);
+  stage_window(dv, zero_line(P, t, lane), hdr, lane);
   vm_wait<0>();
-  return parse_packet<ROWB>(P, reinterpret_cast<const uint8_t*>(&hdr[0][lane]), dv.shift, dv.len,
+  return parse_packet(P, window_of(hdr, lane), dv.shift, dv.len,
                             dv.intf_i, dv.abase, dv.span);
 }
 

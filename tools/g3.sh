@@ -1,5 +1,4 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"; mkdir -p gpurun_out
-S=""
-for v in ${VARS:-noparse s4 s12 s16 ws3 ws1}; do S="$S OO_RX_KERNEL=${KER:-split};OO_RX_LIB=build/var_$v.so"; done
-SWEEP="OO_RX_KERNEL=${KER:-split} $S" CONFIG=${CONFIG:-2} STEPS=100 bash tools/sweep.sh || exit $?
+OO_RX_KERNEL=lanes timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t_lanes.log 2>&1; rc=$?; tail -2 gpurun_out/t_lanes.log; [ $rc -ne 0 ] && exit $rc
+for c in 2 3; do SWEEP="OO_RX_KERNEL=lanes OO_RX_KERNEL=split" CONFIG=$c STEPS=50 bash tools/sweep.sh || exit $?; done
