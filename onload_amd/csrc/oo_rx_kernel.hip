@@ -71,7 +71,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define OO_RX_WS 2  // rx_split: streamer waves per block (plus one parser)
 #endif
 #ifndef OO_RX_SRING
-#define OO_RX_SRING 6  // rx_split: body ring slots per streamer (even)
+#define OO_RX_SRING 4  // rx_split: body ring slots per streamer (even)
 #endif
 
 constexpr int WAVES = OO_RX_WAVES;
@@ -941,61 +941,81 @@ __device__ __forceinline__ uint32_t slot_rounds(const Jobs& J, uint32_t js) {
 
 struct IssueCursor {
   uint32_t js, rnd, R;  // job slot, round in it, its rounds (wave-uniform)
-  uint32_t lv;          // rounds of the slot in which this lane has a chunk
-  uint64_t a;           // this lane's next chunk
+  uint32_t adv;         // rounds after which a stops advancing
+  uint64_t a;           // the chunk this lane reads next
 };
 
-// Point the issue cursor at job slot js (R = 0: past the last).  All lanes
-// active.
+// Point the issue cursor at job slot js (R = 0: past the last).  A lane past
+// its job's end keeps reading the job's last chunk it read; a lane whose
+// group has no job in the slot reads what the same lane of group 0 reads
+// (group 0 has a job in every slot that is not past the last): the same
+// lines as the instruction's live lanes, so no extra HBM traffic, and the
+// consume side masks them.  Only a slot whose group-0 job is shorter than
+// eight chunks leaves lanes on the zero line.  All lanes active.
 __device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32_t js,
-                                           uint32_t lane) {
-  const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
-  const uint32_t nb = lane_get(J.nb, s);
-  const uint32_t lo = lane_get(J.lo, s), hi = lane_get(J.hi, s);
+                                           uint32_t lane, uint64_t zero) {
+  const uint32_t gj = lane & 7u, jj = min(js, 7u), s = (lane & ~7u) + jj;
+  const uint32_t nb = lane_get(J.nb, s), lo = lane_get(J.lo, s), hi = lane_get(J.hi, s);
+  const uint32_t nb0 = lane_get(J.nb, jj), lo0 = lane_get(J.lo, jj), hi0 = lane_get(J.hi, jj);
   c.js = js;
   c.rnd = 0;
   c.R = slot_rounds(J, js);
-  c.lv = (c.R != 0 && nb > gj) ? (nb - gj + 7u) >> 3 : 0u;
-  c.a = ((uint64_t)hi << 32 | lo) + gj * 16u;
+  const bool own = nb > gj, g0 = nb == 0 && nb0 > gj;
+  const uint32_t n = own ? nb : nb0;
+  c.adv = (own || g0) ? (n - gj - 1u) >> 3 : 0u;
+  c.a = c.R == 0 ? zero
+        : own   ? ((uint64_t)hi << 32 | lo) + gj * 16u
+        : g0    ? ((uint64_t)hi0 << 32 | lo0) + gj * 16u
+        : nb != 0 ? ((uint64_t)hi << 32 | lo) + (nb - 1u) * 16u
+                  : zero;
 }
 
-// Issues the cursor's round into `slot` (lanes without a chunk read zeros).
+// Issues the cursor's round into `slot`.
 __device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint64_t zero,
                                             void* slot, uint32_t lane) {
-  glds<OO_RX_BODY_AUX>(c.rnd < c.lv ? c.a : zero, slot);
-  c.a += 128;
-  if (++c.rnd == c.R) issue_slot(c, J, c.js + 1, lane);
+  glds<OO_RX_BODY_AUX>(c.a, slot);
+  c.a += c.rnd < c.adv ? 128u : 0u;
+  if (++c.rnd == c.R) issue_slot(c, J, c.js + 1, lane, zero);
 }
 
 struct ConsumeCursor {
   uint32_t js, rnd, R;  // wave-uniform
+  uint32_t lv;          // rounds of the slot in which this lane has a chunk
   uint32_t acc;         // this lane's running sum
   uint32_t bs;          // the total of job (group, lane & 7); 0 if none
 };
 
-__device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J) {
-  c.js = 0;
+__device__ __forceinline__ void consume_slot(ConsumeCursor& c, const Jobs& J, uint32_t js,
+                                             uint32_t lane) {
+  const uint32_t gj = lane & 7u;
+  const uint32_t nb = lane_get(J.nb, (lane & ~7u) + min(js, 7u));
+  c.js = js;
   c.rnd = 0;
-  c.R = slot_rounds(J, 0);
+  c.R = slot_rounds(J, js);
+  c.lv = (c.R != 0 && nb > gj) ? (nb - gj + 7u) >> 3 : 0u;
+}
+
+__device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, uint32_t lane) {
+  consume_slot(c, J, 0, lane);
   c.acc = 0;
   c.bs = 0;
 }
 
-// Consumes one round from the landed bytes v.
+// Consumes one round from the landed bytes v (lanes past their chunks weigh
+// their words by 0).
 __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
                                               uint32_t lane) {
-  uint32_t a = dot(v.x, 0x00010001u, c.acc);
-  uint32_t b = dot(v.y, 0x00010001u, 0u);
-  a = dot(v.z, 0x00010001u, a);
-  b = dot(v.w, 0x00010001u, b);
+  const uint32_t w = c.rnd < c.lv ? 0x00010001u : 0u;
+  uint32_t a = dot(v.x, w, c.acc);
+  uint32_t b = dot(v.y, w, 0u);
+  a = dot(v.z, w, a);
+  b = dot(v.w, w, b);
   c.acc = a + b;
   if (++c.rnd == c.R) {  // the slot's jobs end: fold each group
     const uint32_t t = group_sum8(c.acc);
     if ((lane & 7u) == c.js) c.bs = t;
     c.acc = 0;
-    ++c.js;
-    c.rnd = 0;
-    c.R = slot_rounds(J, c.js);
+    consume_slot(c, J, c.js + 1, lane);
   }
 }
 
@@ -1193,9 +1213,9 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     T = 0;
 #endif
     IssueCursor ci;
-    issue_slot(ci, J, 0, lane);
+    issue_slot(ci, J, 0, lane, zero);
     ConsumeCursor cc;
-    consume_start(cc, J);
+    consume_start(cc, J, lane);
     // This tile's header windows: older than the previous tile's NST stores
     // (none before the first tile) and the R rounds issued here.
     if (T != 0) {
@@ -1311,7 +1331,14 @@ __device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (*hdr)[64],
                             dv.intf_i, dv.abase, dv.span);
 }
 
+#ifndef OO_RX_SPLIT_MINW
+#define OO_RX_SPLIT_MINW 0  // rx_split: minimum waves per SIMD (caps VGPRs; 0: none)
+#endif
+#if OO_RX_SPLIT_MINW > 0
+__global__ __launch_bounds__((WS + 1) * 64, OO_RX_SPLIT_MINW) void rx_split(KParams P) {
+#else
 __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
+#endif
   __shared__ __attribute__((aligned(16))) uint4 smem[(sizeof(SplitLds) + 15) / 16];
   SplitLds& L = *reinterpret_cast<SplitLds*>(smem);
   const uint32_t wave = threadIdx.x >> 6;
@@ -1357,15 +1384,15 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
       const DescView dv = desc_view(P, d, tile_of(k, i), lane);
       Ji = jobs_setup(dv.abase, dv.span, lane, myslot_i);
       Ti = (Ji.T + 1u) & ~1u;  // whole pairs: a tile starts on an even slot
-      issue_slot(ci, Ji, 0, lane);
       zero_i = zero_line(P, tile_of(k, i), lane);
+      issue_slot(ci, Ji, 0, lane, zero_i);
       issued_i = 0;
     };
     setup(0);
     // consume side: tile phase kc
     Jobs Jc = Ji;
     ConsumeCursor cc;
-    consume_start(cc, Jc);
+    consume_start(cc, Jc, lane);
     uint32_t kc = 0, Tc = Ti, myslot_c = myslot_i, done_c = 0;
     bool ahead = false;                 // the issue side is in tile kc + 1
     uint32_t issued = 0, consumed = 0;  // ring pieces, nulls included
@@ -1402,7 +1429,7 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
       if (!ahead) move_on();
       if (ahead) {
         Jc = Ji;
-        consume_start(cc, Jc);
+        consume_start(cc, Jc, lane);
         Tc = Ti;
         myslot_c = myslot_i;
         ahead = false;
