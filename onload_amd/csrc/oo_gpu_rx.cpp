@@ -124,7 +124,9 @@ struct oo_gpu_rx_ctx {
   uint8_t* d_zero = nullptr;  // oo_rx::ZERO_LINES x 16 B of zeros
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t grid_split = 1024;  // resident blocks of rx_split
-  uint32_t split_min = 512;    // mean bytes per frame from which rx_split runs
+  uint32_t tstep = 8;                // tile size step (KParams::tstep)
+  uint32_t split_min = 0xffffffffu;  // mean bytes per frame from which rx_split runs (never:
+                                     // rx_kernel measured as fast or faster on configs 2-5)
   int kernel_force = -1;       // OO_RX_KERNEL: 0 = rx_kernel, 1 = rx_split
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
   // host-path staging
@@ -457,6 +459,7 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       c->grid_split = std::max<uint32_t>(1, (uint32_t)(b1 * prop.multiProcessorCount) * pct / 100);
   }
   c->split_min = env_u32("OO_RX_SPLIT_MIN", c->split_min);
+  c->tstep = env_u32("OO_RX_TSTEP", 8) == 1 ? 1 : 8;
   if (const char* k = getenv("OO_RX_KERNEL")) {
     if (!strcmp(k, "split")) c->kernel_force = 1;
     if (!strcmp(k, "lanes")) c->kernel_force = 0;
@@ -596,16 +599,22 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   const int split = c->kernel_force >= 0 ? c->kernel_force
                                          : (frames_bytes >= (uint64_t)c->split_min * n ? 1 : 0);
   // Static balanced partition: the W tile-processing waves (rx_split's
-  // streamers) each take k tiles of P.tile <= 64 packets,
-  // k = ceil(n / (64 W)), P.tile = ceil(n / (W k)).  Small batches use
-  // fewer blocks.
+  // streamers) each take K = ceil(n / (64 W)) tiles; NT = W K tiles of tlo or
+  // tlo + 8 packets (multiples of 8, at most 64), the last taking the < 8
+  // left over.  Small batches use fewer blocks.
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block(split);
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full
   const uint32_t cap = split ? c->grid_split : c->grid;
   const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, cap));
   const uint64_t W = (uint64_t)blocks * wpb;
-  const uint64_t k = (n + 64 * W - 1) / (64 * W);
-  P.tile = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (n + W * k - 1) / (W * k)));
+  const uint64_t K = (n + 64 * W - 1) / (64 * W);
+  const uint64_t NT = W * K;
+  const uint64_t step = c->tstep;
+  const uint64_t tlo = std::min<uint64_t>(64 - step, (n / NT) / step * step);
+  P.ntiles = (uint32_t)NT;
+  P.tlo = (uint32_t)tlo;
+  P.ta = (uint32_t)std::min<uint64_t>(NT, (n - tlo * NT) / step);
+  P.tstep = (uint32_t)step;
   const int grid = (int)blocks;
   return oo_rx_launch(&P, split, grid, s) == 0 ? 0 : -EIO;
 }

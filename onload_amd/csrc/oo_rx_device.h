@@ -78,7 +78,10 @@ struct KParams {
   oo_gpu_rx_result* out;
   uint32_t* counters;  // OO_RX_R_COUNT u32, may be null
   uint32_t n;
-  uint32_t tile;  // packets per tile (1..64)
+  uint32_t ntiles;  // tiles (oo_rx_kernel.hip "Tiles")
+  uint32_t tlo;     // tile sizes: tlo + tstep for tiles < ta, else tlo (the last: the rest)
+  uint32_t ta;
+  uint32_t tstep;   // 8 (job slots fill), or 1 (OO_RX_TSTEP=1: sizes within one packet)
   uint32_t ip4_mask;
   uint32_t ip6_mask;
   const Slot4* slot4;

@@ -238,12 +238,13 @@ __device__ __forceinline__ uint32_t group_sum8(uint32_t v) {
 }
 
 // The body stream of the frame (see "Body streaming engine") whose window starts at abase (span window bytes):
-// off0 = a0 - abase, in (0, HB], a multiple of 16, and its whole chunks.
+// off0 = a0 - abase, in (0, HB], a multiple of 16, and its chunks (the last
+// may be partial).
 __device__ __forceinline__ uint32_t body_off0(uint64_t abase) {
   return (uint32_t)(((abase + HB) & ~(uint64_t)127) - abase);
 }
 __device__ __forceinline__ uint32_t body_chunks(uint32_t off0, int span) {
-  return span > HB ? (((uint32_t)span & ~15u) - off0) >> 4 : 0u;
+  return span > HB ? ((uint32_t)span - off0 + 15u) >> 4 : 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -385,11 +386,10 @@ struct Hdr {
 };
 
 // A packet's staged window in LDS (stage_window): a 128-B row whose 16-B
-// cell k sits at row + 16 * ((k + rot) & 7), and the frame's last chunk.
+// cell k sits at row + 16 * ((k + rot) & 7).
 struct Win {
   const uint8_t* row;
   uint32_t rot;
-  const uint8_t* tail;
   __device__ __forceinline__ const uint8_t* cell(int k) const {
     return row + ((((uint32_t)k + rot) & 7u) << 4);
   }
@@ -807,21 +807,9 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, i
   ps.r = r;
   ps.s4 = h.s4;
   ps.pseudo = h.pseudo;
-  // The body stream covers the whole chunks of window bytes [off0, span);
-  // the frame's last partial chunk (staged in cell HC) is summed here, and
-  // an L4 region that ends before the frame does leaves its complement to
-  // subtract.
-  if (h.longl4) {
-    if (span & 15) {
-      uint4 t;
-      asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
-                   : "=v"(t)
-                   : "v"((uint32_t)(uintptr_t)(lptr)(W.tail)), "n"(0)
-                   : "memory");
-      ps.s4 += chunk_sum(t, span & ~15, span & ~15, span);
-    }
-    if (h.E4 < span) ps.s4 -= window_sum_global(abase, h.E4, span);
-  }
+  // The body stream covers window bytes [off0, span); an L4 region that
+  // ends before the frame does leaves its complement to subtract.
+  if (h.longl4 && h.E4 < span) ps.s4 -= window_sum_global(abase, h.E4, span);
   ps.odd_long = (uint32_t)(shift & 1) | (h.longl4 ? 2u : 0u);
   return ps;
 }
@@ -853,10 +841,9 @@ __device__ __forceinline__ void store_record(const KParams& P, uint32_t idx,
 // ---------------------------------------------------------------------------
 // Body streaming engine.
 //
-// A frame's body is its whole 16-B chunks from a0, the 128-B line holding
-// window byte HB, up to the frame end rounded down to 16 B.  The parse covers
-// the rest of the L4 region: the window bytes before a0, and the frame's last
-// partial chunk, which is staged with the header window (cell HC).
+// A frame's body is its 16-B chunks from a0, the 128-B line holding window
+// byte HB, to the frame end (the last chunk may be partial).  The parse covers
+// the window bytes before a0.
 //
 // The tile's frames with a body are its jobs.  Job q goes to lane (g, j) =
 // (q & 7, q >> 3); 8-lane group g streams its jobs j = 0, 1, ... one after
@@ -866,13 +853,15 @@ __device__ __forceinline__ void store_record(const KParams& P, uint32_t idx,
 // tools/ring_probe.hip).  All groups move to the next job slot on the same
 // round: slot j lasts R_j rounds, the most any of its eight jobs needs.  When
 // the tile's frames differ in size they are first ranked by size, so the jobs
-// of a slot are alike.  Lanes past their job's end read zeros, so consuming a
-// round is four dot products and no masking, and the job/slot bookkeeping is
-// scalar.
+// of a slot are alike.  Consuming a round is four dot products with a
+// per-lane word weight (0 for lanes past their job's end); a job's partial
+// last chunk takes a masked sum in the round that holds it.  The job/slot
+// bookkeeping is scalar.
 
 struct Jobs {       // a tile's jobs: lane (g, j) holds job q = g + 8 j
   uint32_t lo, hi;  // a0
-  uint32_t nb;      // whole chunks from a0 (0: no job)
+  uint32_t nb;      // chunks from a0 (0: no job)
+  uint32_t lim;     // frame end relative to a0
   uint32_t rj;      // R_(lane & 7): rounds of that job slot
   uint32_t T;       // rounds of the tile
 };
@@ -925,6 +914,7 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
   J.lo = lane_get((uint32_t)a0, jp);
   J.hi = lane_get((uint32_t)(a0 >> 32), jp);
   J.nb = lane_get(nb, jp);
+  J.lim = lane_get((uint32_t)span - off0, jp);
   // R_j: the most rounds over lanes 8g + j
   uint32_t m = (J.nb + 7u) >> 3;
   m = max(m, lane_get(m, lane ^ 8u));
@@ -981,18 +971,27 @@ __device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint6
 struct ConsumeCursor {
   uint32_t js, rnd, R;  // wave-uniform
   uint32_t lv;          // rounds of the slot in which this lane has a chunk
+  uint32_t vb;          // bytes of its last chunk in the frame (1..16)
+  uint4 m;              // byte mask of its last chunk
   uint32_t acc;         // this lane's running sum
   uint32_t bs;          // the total of job (group, lane & 7); 0 if none
 };
 
 __device__ __forceinline__ void consume_slot(ConsumeCursor& c, const Jobs& J, uint32_t js,
                                              uint32_t lane) {
-  const uint32_t gj = lane & 7u;
-  const uint32_t nb = lane_get(J.nb, (lane & ~7u) + min(js, 7u));
+  const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
+  const uint32_t nb = lane_get(J.nb, s), lim = lane_get(J.lim, s);
   c.js = js;
   c.rnd = 0;
   c.R = slot_rounds(J, js);
   c.lv = (c.R != 0 && nb > gj) ? (nb - gj + 7u) >> 3 : 0u;
+  const int last = 16 * (int)(gj + 8u * (c.lv - 1u));  // this lane's last chunk
+  c.vb = (uint32_t)min(max((int)lim - last, 0), 16);
+  auto bytes = [](int k) -> uint32_t {
+    return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * k)) - 1u;
+  };
+  const int vb = (int)c.vb;
+  c.m = make_uint4(bytes(vb), bytes(vb - 4), bytes(vb - 8), bytes(vb - 12));
 }
 
 __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, uint32_t lane) {
@@ -1005,12 +1004,25 @@ __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, u
 // their words by 0).
 __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
                                               uint32_t lane) {
-  const uint32_t w = c.rnd < c.lv ? 0x00010001u : 0u;
-  uint32_t a = dot(v.x, w, c.acc);
-  uint32_t b = dot(v.y, w, 0u);
-  a = dot(v.z, w, a);
-  b = dot(v.w, w, b);
-  c.acc = a + b;
+  const bool live = c.rnd < c.lv;
+  const bool part = live && c.rnd + 1u == c.lv && c.vb != 16u;
+  if (__ballot(part) == 0) {
+    const uint32_t w = live ? 0x00010001u : 0u;
+    uint32_t a = dot(v.x, w, c.acc);
+    uint32_t b = dot(v.y, w, 0u);
+    a = dot(v.z, w, a);
+    b = dot(v.w, w, b);
+    c.acc = a + b;
+  } else {  // some lane holds a frame's partial last chunk: byte masks
+    // (an odd end leaves the last word's high byte 0, as the reference pads)
+    const uint32_t f = live ? 0xffffffffu : 0u;
+    const uint4 mm = part ? c.m : make_uint4(f, f, f, f);
+    uint32_t a = dot(v.x & mm.x, 0x00010001u, c.acc);
+    uint32_t b = dot(v.y & mm.y, 0x00010001u, 0u);
+    a = dot(v.z & mm.z, 0x00010001u, a);
+    b = dot(v.w & mm.w, 0x00010001u, b);
+    c.acc = a + b;
+  }
   if (++c.rnd == c.R) {  // the slot's jobs end: fold each group
     const uint32_t t = group_sum8(c.acc);
     if ((lane & 7u) == c.js) c.bs = t;
@@ -1019,11 +1031,34 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
   }
 }
 
-// A tile's zero lines: 1 KiB of the zero region per tile, so the lanes that
+// Tiles.  The batch is cut into P.ntiles tiles, K per tile-processing wave
+// (rx_kernel's waves, rx_split's streamers), which take tiles w, w + W, ...
+// (all waves sweep the buffer together: reading one ~200-MB window at a time
+// is faster than 2560 separate contiguous ranges).  Tile sizes are multiples
+// of 8 -- tlo or tlo + 8 packets, the last tile taking the < 8 left over --
+// so the body stream's job slots fill (a slot holds 8 jobs).
+struct Unit {
+  uint32_t first, cnt;  // packets [first, first + cnt)
+  uint32_t key;         // spreads the tile's zero lines
+};
+__device__ __forceinline__ Unit unit_of(const KParams& P, uint32_t t) {
+  Unit u;
+  u.key = t;
+  if (t >= P.ntiles) {
+    u.first = 0;
+    u.cnt = 0;
+    return u;
+  }
+  u.first = P.tlo * t + P.tstep * min(t, P.ta);
+  u.cnt = t + 1u == P.ntiles ? P.n - u.first : P.tlo + (t < P.ta ? P.tstep : 0u);
+  return u;
+}
+
+// A unit's zero lines: 1 KiB of the zero region per unit, so the lanes that
 // read zeros are spread over the L2 channels.
-__device__ __forceinline__ uint64_t zero_line(const KParams& P, uint32_t tile, uint32_t lane) {
+__device__ __forceinline__ uint64_t zero_line(const KParams& P, const Unit& t, uint32_t lane) {
   return reinterpret_cast<uint64_t>(P.zero) +
-         (uint64_t)(((tile * 64u + lane) & (ZERO_LINES - 1u)) * 16u);
+         (uint64_t)(((t.key * 64u + lane) & (ZERO_LINES - 1u)) * 16u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1036,11 +1071,11 @@ struct DescView {
   bool valid;
   uint32_t idx;
 };
-__device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, uint32_t tile,
+__device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, const Unit& t,
                                               uint32_t lane) {
   DescView v;
-  v.idx = tile * P.tile + lane;
-  v.valid = lane < P.tile && v.idx < P.n;
+  v.idx = t.first + lane;
+  v.valid = lane < t.cnt;
   const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
   int len = (int)(d.z & 0xffffu);
   v.intf_i = (int)(int16_t)(d.z >> 16);
@@ -1054,11 +1089,11 @@ __device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, 
   return v;
 }
 
-__device__ __forceinline__ uint64_t desc_src(const KParams& P, uint32_t tile, uint32_t lane,
-                                             uint32_t ntiles) {
-  const uint32_t i = tile * P.tile + lane;
+// Where lane `lane` of unit t loads its descriptor from (lanes without a
+// packet: some other in-bounds entry).
+__device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, uint32_t lane) {
   return reinterpret_cast<uint64_t>(P.desc) +
-         (uint64_t)((tile < ntiles && lane < P.tile && i < P.n) ? i : lane % P.n) * 16;
+         (uint64_t)(lane < t.cnt ? t.first + lane : lane % P.n) * 16;
 }
 
 // Per-reason counters: one global atomic per distinct reason in the wave
@@ -1081,9 +1116,8 @@ __device__ __forceinline__ void count_reasons(const KParams& P, bool valid, uint
 // its cell k at 16 * ((k - p) & 7) within it, so one LDS-DMA instruction
 // reads eight packets' windows, eight lanes (one 128-B run) per packet --
 // 8-16 cache lines per instruction, not 64 -- and the packet-per-lane reads
-// of any one cell fall in distinct banks.  Row HC holds each frame's last
-// partial chunk when it lies past the window (lane = packet).  Chunks a frame
-// does not have read zeros.  All lanes active.
+// of any one cell fall in distinct banks.  Chunks a frame does not have read
+// zeros.  All lanes active.
 __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64],
                                              uint32_t lane) {
   const uint32_t lo = (uint32_t)dv.abase, hi = (uint32_t)(dv.abase >> 32);
@@ -1095,15 +1129,12 @@ __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, 
     const int nwin = ((int)lane_get((uint32_t)dv.span, p) + 15) >> 4;
     glds<OO_RX_HDR_AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
   }
-  const bool tail = dv.span > HB && (dv.span & 15) != 0;
-  glds<OO_RX_HDR_AUX>(tail ? dv.abase + (uint64_t)(dv.span & ~15) : zero, &rows[HC][0]);
 }
 
 __device__ __forceinline__ Win window_of(uint4 (*rows)[64], uint32_t lane) {
   Win W;
   W.row = reinterpret_cast<const uint8_t*>(&rows[0][0]) + 128u * lane;
   W.rot = (8u - (lane & 7u)) & 7u;
-  W.tail = reinterpret_cast<const uint8_t*>(&rows[HC][lane]);
   return W;
 }
 
@@ -1113,15 +1144,15 @@ __device__ __forceinline__ Win window_of(uint4 (*rows)[64], uint32_t lane) {
 // descriptors of the tile after it) land in LDS, so each tile starts with its
 // headers in place.  A wave's vector-memory operations (loads, LDS-DMA,
 // stores) retire in issue order, and every wait counts the operations issued
-// after the ones it needs: NHS staging operations per tile (HC + 1 header rows
-// and one descriptor line) and NST record stores, both issued by the whole
+// after the ones it needs: NHS staging operations per tile (HC header rows and
+// one descriptor line) and NST record stores, both issued by the whole
 // wave whatever its lanes hold, so the counts are static.
 
-constexpr int NHS = HC + 2;
+constexpr int NHS = HC + 1;
 constexpr int NST = 2;
 
 struct WaveLds {
-  uint4 hdr[HC + 1][64];        // header windows (stage_window)
+  uint4 hdr[HC][64];            // header windows (stage_window)
   uint4 ring[R][64];            // body ring: slot = one round of the eight groups
   uint4 desc[2][64];            // descriptors of this tile and of the next
   uint32_t cnt[OO_RX_R_COUNT];  // per-reason counts
@@ -1180,28 +1211,28 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
   const uint32_t lane = threadIdx.x & 63u;
   WaveLds& L = reinterpret_cast<WaveLds*>(smem)[wave];
 
-  const uint32_t ntiles = (P.n + P.tile - 1) / P.tile;
-  const uint32_t stride = gridDim.x * WAVES;
-  uint32_t tile = blockIdx.x * WAVES + wave;
-  if (tile >= ntiles) return;
   const uint32_t gwave = blockIdx.x * WAVES + wave;
-  (void)gwave;
+  const uint32_t W = gridDim.x * WAVES;
+  const uint32_t K = (P.ntiles - gwave + W - 1) / W;  // this wave's tiles gwave + k W
+  if (gwave >= P.ntiles) return;
   if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
 
   // Prologue: this tile's descriptors, then the next tile's and this tile's
   // header windows.
-  glds<0>(desc_src(P, tile, lane, ntiles), &L.desc[0][0]);
+  const Unit t0 = unit_of(P, gwave);
+  glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
   vm_wait<0>();
-  glds<0>(desc_src(P, tile + stride, lane, ntiles), &L.desc[1][0]);
+  glds<0>(desc_src(P, unit_of(P, gwave + W), lane), &L.desc[1][0]);
   {
-    const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), tile, lane);
-    stage_window(d0, zero_line(P, tile, lane), L.hdr, lane);
+    const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
+    stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
   }
 
   uint32_t b = 0, it_ = 0;
-  for (; tile < ntiles; tile += stride, b ^= 1u, ++it_) {
+  for (; it_ < K; b ^= 1u, ++it_) {
     STAMP(0, __builtin_amdgcn_s_memrealtime());
-    STAMP(6, tile);
+    const Unit tile = unit_of(P, gwave + it_ * W);
+    STAMP(6, tile.first);
     const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), tile, lane);
     const uint64_t zero = zero_line(P, tile, lane);
 
@@ -1242,9 +1273,9 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
 
     // ---- stage the next tile: descriptors of the tile after it into this
     // tile's buffer, and its header windows.
-    glds<0>(desc_src(P, tile + 2u * stride, lane, ntiles), &L.desc[b][0]);
+    glds<0>(desc_src(P, unit_of(P, gwave + (it_ + 2u) * W), lane), &L.desc[b][0]);
     {
-      const uint32_t nt = tile + stride;
+      const Unit nt = unit_of(P, gwave + (it_ + 1u) * W);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
     }
@@ -1307,7 +1338,7 @@ struct StreamerLds {
 };
 struct SplitLds {
   StreamerLds s[WS];
-  uint4 hdr[HC + 1][64];  // the parser's header window + last chunks, [chunk][packet]
+  uint4 hdr[HC][64];  // the parser's header windows (stage_window)
 };
 static_assert(SR >= 2 && SR % 2 == 0, "a streamer consumes its ring two pieces at a time");
 
@@ -1319,11 +1350,10 @@ __device__ __forceinline__ void block_barrier() {
 
 // The parser's header work for tile t: the window staged by LDS-DMA (lane
 // = packet, [chunk][packet] cells, as in rx_kernel), then the common parse.
-__device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (*hdr)[64], uint32_t t,
+__device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (*hdr)[64], const Unit& t,
                                              uint32_t lane) {
-  const uint32_t idx = t * P.tile + lane;
   uint4 d = make_uint4(0, 0, 0, 0);
-  if (lane < P.tile && idx < P.n) d = *reinterpret_cast<const uint4*>(P.desc + idx);
+  if (lane < t.cnt) d = *reinterpret_cast<const uint4*>(P.desc + t.first + lane);
   const DescView dv = desc_view(P, d, t, lane);
   stage_window(dv, zero_line(P, t, lane), hdr, lane);
   vm_wait<0>();
@@ -1343,10 +1373,9 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
   SplitLds& L = *reinterpret_cast<SplitLds*>(smem);
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t ntiles = (P.n + P.tile - 1) / P.tile;
   const uint32_t G = gridDim.x;
-  const uint32_t K = (ntiles + G * WS - 1) / (G * WS);  // tile phases
-  auto tile_of = [&](uint32_t k, uint32_t i) { return (k * G + blockIdx.x) * WS + i; };
+  const uint32_t K = (P.ntiles + G * WS - 1) / (G * WS);  // tile phases
+  auto tile_of = [&](uint32_t k, uint32_t i) { return unit_of(P, (k * G + blockIdx.x) * WS + i); };
 #ifdef OO_RX_STAMPS
   // Diagnostic: stamps[((block * (WS + 1) + wave) * 64 + phase) * 8 + slot].
   auto sstamp = [&](uint32_t k, int ph, uint64_t val) {
@@ -1371,7 +1400,7 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
     // ring), so every wait is the same vmcnt(SR-2).
     StreamerLds& S = L.s[wave];
     const uint32_t i = wave;
-    glds<0>(desc_src(P, tile_of(0, i), lane, ntiles), &S.desc[0][0]);
+    glds<0>(desc_src(P, tile_of(0, i), lane), &S.desc[0][0]);
     vm_wait<0>();
 
     // issue side: tile ti, its jobs and cursor
@@ -1399,8 +1428,8 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
     // Descriptors of tile t are fetched at the end of phase t - 3; a piece
     // issued after them that has been consumed proves they landed.
     uint32_t mark_prev = 0, mark_new = 0;
-    if (K > 1) glds<0>(desc_src(P, tile_of(1, i), lane, ntiles), &S.desc[1][0]);
-    if (K > 2) glds<0>(desc_src(P, tile_of(2, i), lane, ntiles), &S.desc[2][0]);
+    if (K > 1) glds<0>(desc_src(P, tile_of(1, i), lane), &S.desc[1][0]);
+    if (K > 2) glds<0>(desc_src(P, tile_of(2, i), lane), &S.desc[2][0]);
 
     auto move_on = [&]() {  // the issue side enters tile ti + 1
       if (ahead || ti + 1 >= K) return;
@@ -1443,7 +1472,7 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
       SSTAMP(kc, 3);
       ++kc;
       if (kc + 2 < K) {
-        glds<0>(desc_src(P, tile_of(kc + 2, i), lane, ntiles), &S.desc[(kc + 2) % 3][0]);
+        glds<0>(desc_src(P, tile_of(kc + 2, i), lane), &S.desc[(kc + 2) % 3][0]);
         mark_prev = mark_new;
         mark_new = issued;
       }
@@ -1484,11 +1513,11 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
       if (k > 0) {
 #pragma unroll
         for (int i = 0; i < WS; ++i) {
-          const uint32_t t = tile_of(k - 1, (uint32_t)i);
-          if (t < ntiles) {
+          const Unit t = tile_of(k - 1, (uint32_t)i);
+          if (t.cnt != 0) {
             finish(ps[i], L.s[i].bsum[(k - 1) & 1][lane]);
-            const uint32_t idx = t * P.tile + lane;
-            const bool valid = lane < P.tile && idx < P.n;
+            const uint32_t idx = t.first + lane;
+            const bool valid = lane < t.cnt;
             count_reasons(P, valid, ps[i].r.reason);
             if (valid) store_record(P, idx, ps[i].r);
           }
@@ -1498,11 +1527,11 @@ __global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
       if (k < K) {
 #pragma unroll
         for (int i = 0; i < WS; ++i) {
-          const uint32_t t = tile_of(k, (uint32_t)i);
+          const Unit t = tile_of(k, (uint32_t)i);
 #ifdef OO_RX_ABL_NOPARSE
-          if (t < ntiles) ps[i] = Parsed{};
+          if (t.cnt != 0) ps[i] = Parsed{};
 #else
-          if (t < ntiles) ps[i] = parse_tile(P, L.hdr, t, lane);
+          if (t.cnt != 0) ps[i] = parse_tile(P, L.hdr, t, lane);
 #endif
         }
       }

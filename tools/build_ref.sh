@@ -1,0 +1,15 @@
+#!/bin/bash
+# Builds the product library of git revision REV (default HEAD) as
+# build/var_<NAME>.so (default NAME=ref), for same-box A/B sweeps
+# (OO_RX_LIB=build/var_ref.so) -- run-to-run differences between GPU boxes
+# are a few percent, more than many of the changes being measured.
+set -eu
+REV="${1:-HEAD}"; NAME="${2:-ref}"
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+T=$(mktemp -d)
+git -C "$ROOT" archive "$REV" onload_amd/csrc include | tar -x -C "$T"
+mkdir -p "$ROOT/build"
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -shared \
+  -o "$ROOT/build/var_$NAME.so" "$T/onload_amd/csrc/oo_rx_kernel.hip" "$T/onload_amd/csrc/oo_gpu_rx.cpp"
+rm -rf "$T"
+echo "build/var_$NAME.so <- $REV"
