@@ -115,6 +115,33 @@ def test_config_samples(cuda, config, n):
         assert set(np.unique(got["stage"][r == 0]).tolist()) == {1, 2, 3}
 
 
+@pytest.mark.parametrize("n", [1, 7, 9, 63, 65, 1000, 20001])
+def test_ragged_batch_sizes(cuda, n):
+    """Tile partition edges: batches far below one tile per wave, sizes that
+    are not multiples of 8 (the last tile takes the rest)."""
+    filters, socks = pktgen.world(4)
+    g, o = _pair(lambda s: s.load_world(filters, socks))
+    buf, desc = pktgen.generate(4, n, first=777)
+    _check(g, o, buf, desc)
+
+
+@pytest.mark.parametrize("case", ["edge0", "edge1", "config2", "config4"])
+def test_split_kernel(cuda, monkeypatch, case):
+    """rx_split (one parser + two streamer waves per block), the library's
+    other kernel, against the oracle."""
+    monkeypatch.setenv("OO_RX_KERNEL", "split")
+    if case.startswith("edge"):
+        shift = int(case[-1])
+        g, o = _pair(lambda s: install(s, edge_world()), intf_hwport=HWPORTS)
+        buf, desc = pack(edge_frames(), align=64 if shift % 2 == 0 else 16, shift=shift)
+    else:
+        config = int(case[-1])
+        filters, socks = pktgen.world(config)
+        g, o = _pair(lambda s: s.load_world(filters, socks))
+        buf, desc = pktgen.generate(config, 1 << 15, first=4242)
+    _check(g, o, buf, desc)
+
+
 def test_host_path_matches_device_path(cuda):
     filters, socks = pktgen.world(5)
     buf, desc = pktgen.generate(5, 4096)
