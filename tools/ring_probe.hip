@@ -143,7 +143,7 @@ static void run_grp(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
   const size_t nframes = (bytes - 4096) / FB / 64 * 64;
   int bpc = 0;
   (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, ring_grp<R, G, FB, AL>, 64, lds);
-  for (int m : {4, 8, 12, 16}) {
+  for (int m : {4, 8, 10, 12, 16}) {
     if (m > bpc) break;
     const int grid = cu * m;
     hipEvent_t e0, e1;
@@ -179,8 +179,7 @@ int main(int argc, char** argv) {
     run<16, 1>(a, bytes, o, cu);
     run<32, 1>(a, bytes, o, cu);
   }
-  run_grp<6, 8, 1514>(a, bytes, o, cu);
-  run_grp<6, 8, 1514, true>(a, bytes, o, cu);
-  run_grp<8, 8, 1514, true>(a, bytes, o, cu);
+  run_grp<4, 8>(a, bytes, o, cu);
+  run_grp<6, 8>(a, bytes, o, cu);
   return 0;
 }
