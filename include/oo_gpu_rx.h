@@ -226,6 +226,21 @@ int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* ctx, const void* d_frames,
  * descriptors host->device, runs the transform, copies results (and the
  * per-reason deltas, if `delta` is not NULL) back, and waits.  Frame bytes
  * and n must fit the staging sizes given at open.  Returns n or -errno. */
+/* TX checksum fill on HBM-resident frames, in place, asynchronous on
+ * `stream`: for each descriptor, oo_pkt_calc_checksums
+ * (src/lib/transport/ip/pkt_checksum.c:20-102) as calc_csum_if_needed
+ * (src/lib/transport/ip/netif_tx.c:24-40) runs it on the AF_XDP TX path --
+ * TCP and UDP frames only (one 802.1Q tag parsed as on RX): the IPv4 header
+ * checksum (ef_ip_checksum, src/lib/ciul/checksum.c:185-212), then the UDP
+ * check field (ef_udp_checksum{,_ip6}, :225-250; not for an IPv4 fragment;
+ * 0 is sent as 0xffff) or the TCP one (ef_tcp_checksum{,_ip6}, :260-296)
+ * over the L4 header and the rest of the frame.  Frames whose headers do not
+ * fit, with IHL < 5 or TCP doff < 5 are left as they are where the
+ * reference would assert.  The table state of ctx is not used.
+ * Returns 0 or -errno. */
+int oo_gpu_tx_fill_dev(oo_gpu_rx_ctx* ctx, void* d_frames, uint64_t frames_bytes,
+                       const oo_gpu_pkt_desc* d_desc, uint32_t n, void* stream);
+
 int oo_gpu_rx_batch(oo_gpu_rx_ctx* ctx, const void* frames,
                     uint64_t frames_bytes, const oo_gpu_pkt_desc* desc,
                     uint32_t n, oo_gpu_rx_result* out,

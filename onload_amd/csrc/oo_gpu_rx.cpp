@@ -28,6 +28,7 @@
 #include "oo_rx_device.h"
 
 extern "C" int oo_rx_launch(const oo_rx::KParams* P, int split, int grid, hipStream_t stream);
+extern "C" int oo_tx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_rx_blocks_per_cu(int split);
 extern "C" int oo_rx_waves_per_block(int split);
 
@@ -573,9 +574,10 @@ int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   return sync_tables(c, static_cast<hipStream_t>(stream));
 }
 
+// tx: the TX checksum fill (tx_kernel) instead of the RX transform.
 static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
                   const oo_gpu_pkt_desc* d_desc, uint32_t n, oo_gpu_rx_result* d_out,
-                  uint32_t* d_ctr, hipStream_t s) {
+                  uint32_t* d_ctr, hipStream_t s, bool tx = false) {
   KParams P;
   memset(&P, 0, sizeof(P));
   P.frames = static_cast<const uint8_t*>(d_frames);
@@ -596,8 +598,9 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
   // rx_split (parser + streamer waves) for large frames, rx_kernel otherwise;
   // the frame buffer's bytes per descriptor estimate the mean frame size.
-  const int split = c->kernel_force >= 0 ? c->kernel_force
-                                         : (frames_bytes >= (uint64_t)c->split_min * n ? 1 : 0);
+  const int split = tx ? 0
+                 : c->kernel_force >= 0 ? c->kernel_force
+                                        : (frames_bytes >= (uint64_t)c->split_min * n ? 1 : 0);
   // Static balanced partition: the W tile-processing waves (rx_split's
   // streamers) each take K = ceil(n / (64 W)) tiles; NT = W K tiles of tlo or
   // tlo + 8 packets (multiples of 8, at most 64), the last taking the < 8
@@ -616,6 +619,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.ta = (uint32_t)std::min<uint64_t>(NT, (n - tlo * NT) / step);
   P.tstep = (uint32_t)step;
   const int grid = (int)blocks;
+  if (tx) return oo_tx_launch(&P, grid, s) == 0 ? 0 : -EIO;
   return oo_rx_launch(&P, split, grid, s) == 0 ? 0 : -EIO;
 }
 
@@ -632,6 +636,16 @@ int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frame
   if (rc) return rc;
   return launch(c, d_frames, frames_bytes, d_desc, n, d_out,
                 reinterpret_cast<uint32_t*>(d_counters), s);
+}
+
+int oo_gpu_tx_fill_dev(oo_gpu_rx_ctx* c, void* d_frames, uint64_t frames_bytes,
+                       const oo_gpu_pkt_desc* d_desc, uint32_t n, void* stream) {
+  if (c == nullptr || (n > 0 && (d_frames == nullptr || d_desc == nullptr))) return -EINVAL;
+  if (c->device < 0) return -ENODEV;
+  if (n == 0) return 0;
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  return launch(c, d_frames, frames_bytes, d_desc, n, nullptr, nullptr,
+                static_cast<hipStream_t>(stream), true);
 }
 
 int oo_gpu_rx_batch(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes,

@@ -81,7 +81,6 @@ constexpr int WS = OO_RX_WS;
 constexpr int SR = OO_RX_SRING;
 constexpr int HC = 8;                // staged header chunks per packet
 constexpr int HB = HC * 16;          // staged window bytes per packet
-constexpr int ROWB = 64 * 16;        // one staged chunk of all 64 packets (LDS-DMA rows)
 
 // Filter-table entry states (netif_table.c:34-42).
 constexpr uint32_t ST_MASK = 0xc0000000u;
@@ -1139,6 +1138,137 @@ __device__ __forceinline__ Win window_of(uint4 (*rows)[64], uint32_t lane) {
 }
 
 // ---------------------------------------------------------------------------
+// TX checksum fill: oo_pkt_calc_checksums
+// (src/lib/transport/ip/pkt_checksum.c:20-102) as calc_csum_if_needed
+// (netif_tx.c:24-40) calls it, on the same streaming engine.  Only TCP and
+// UDP frames: the IPv4 header checksum (ef_ip_checksum, checksum.c:185-212),
+// then the L4 check field over the L4 header and the rest of the frame
+// (ef_udp_checksum{,_ip6} checksum.c:225-250, not for an IPv4 fragment;
+// ef_tcp_checksum{,_ip6} checksum.c:260-296).  The L4 sum here covers the
+// whole L4 region including the old check field, and the pseudo-header term
+// carries 0xffff - old check, which is what the reference's TCP code does and
+// is the same value mod 0xffff as the UDP code's skipping of the field; both
+// sums are non-zero (the pseudo-header holds the protocol), so the folds
+// agree.  A frame whose headers do not fit, or with IHL < 5 or TCP doff < 5,
+// keeps its L4 check field (and, when the IPv4 header itself does not fit or
+// has IHL < 5, its IP check field) -- the reference asserts those away.
+
+struct TxHdr {
+  uint32_t ip_pos, l4_pos;  // frame offsets of the check fields
+  uint32_t ip_ck;           // the IPv4 header checksum to store
+  bool ip_do, l4_do, udp, longl4;
+  uint32_t s4;      // window part of the L4 region's word sum (window coordinates)
+  uint32_t pseudo;  // pseudo-header words + 0xffff - old check (L4-relative)
+};
+
+__device__ __forceinline__ TxHdr tx_header(const Win& W, int shift, int len, uint64_t abase) {
+  auto B = [&](int j) -> uint32_t {
+    int w = shift + j;
+    w = w < HB ? w : HB - 1;
+    const uint32_t v = W.cell(w >> 4)[w & 15];
+    return j < len ? v : 0u;
+  };
+  auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
+  auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
+  TxHdr h;
+  h.ip_do = h.l4_do = h.udp = h.longl4 = false;
+  h.ip_pos = h.l4_pos = h.ip_ck = h.s4 = h.pseudo = 0;
+  if (len < 14) return h;
+  const int l3 = BE16(12) == 0x8100u ? 18 : 14;  // ci_parse_rx_vlan
+  const uint32_t et = BE16(l3 - 2);
+  const bool af6 = et == 0x86ddu;
+  if (!af6 && et != 0x0800u) return h;
+  int ihl4 = 40;
+  uint32_t proto;
+  if (!af6) {
+    if (len < l3 + 20) return h;
+    ihl4 = (int)(B(l3) & 0xfu) * 4;
+    if (ihl4 < 20 || len < l3 + ihl4) return h;
+    proto = B(l3 + 9);
+  } else {
+    if (len < l3 + 40) return h;
+    proto = B(l3 + 6);
+  }
+  if (proto != 6u && proto != 17u) return h;
+  const int l4 = l3 + ihl4;
+  if (!af6) {  // ef_ip_checksum: the header words without the check field
+    uint32_t s = 0;
+    for (int k = 0; k < ihl4; k += 2) s += k == 10 ? 0u : N16(l3 + k);
+    h.ip_do = true;
+    h.ip_pos = (uint32_t)(l3 + 10);
+    h.ip_ck = (~fold16(s)) & 0xffffu;
+  }
+  uint32_t pseudo = 0;
+  int ck;
+  if (proto == 17u) {
+    if (!af6 && (BE16(l3 + 6) & ~0x4000u) != 0) return h;  // ci_ipx_is_frag
+    if (len < l4 + 8) return h;
+    ck = l4 + 6;
+    pseudo = 0x1100u + N16(l4 + 4);
+  } else {
+    if (len < l4 + 20) return h;
+    const int hl4 = (int)(B(l4 + 12) >> 4) * 4;
+    if (hl4 < 20 || len < l4 + hl4) return h;
+    ck = l4 + 16;
+    if (af6) {
+      pseudo = 0x0600u + N16(l3 + 4);
+    } else {
+      const uint32_t pl = (BE16(l3 + 2) - (uint32_t)ihl4) & 0xffffu;
+      pseudo = 0x0600u + (((pl & 0xffu) << 8) | (pl >> 8));
+    }
+  }
+  if (af6) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pseudo += N16(l3 + 8 + 2 * i);
+  } else {
+    pseudo += N16(l3 + 12) + N16(l3 + 14) + N16(l3 + 16) + N16(l3 + 18);
+  }
+  h.pseudo = pseudo + (0xffffu - N16(ck));
+  h.l4_do = true;
+  h.udp = proto == 17u;
+  h.l4_pos = (uint32_t)ck;
+  // The L4 region is [l4, len): its window part, as on RX (the body stream
+  // covers [off0, span) when the region runs past the window).
+  const int off0 = (int)body_off0(abase);
+  const int S4 = shift + l4, E4 = shift + len;
+  h.longl4 = E4 > HB;
+  const int cut = h.longl4 ? off0 : E4;
+  const int lo4 = min(S4, cut), hi4 = max(S4, cut);
+  uint32_t s4 = 0;
+#pragma unroll
+  for (int k = 0; k < HC; ++k) {
+    if (k * 16 < hi4) s4 += chunk_sum(*reinterpret_cast<const uint4*>(W.cell(k)), k * 16, lo4, hi4);
+  }
+  h.s4 = cut < S4 ? 0u - s4 : s4;
+  return h;
+}
+
+// The L4 check value from the window part, the body sum and the
+// pseudo-header term (ip_proto_csum64_finish; UDP 0 -> 0xffff).
+__device__ __forceinline__ uint32_t tx_l4_check(const TxHdr& h, int shift, uint32_t body) {
+  uint32_t f = fold16(h.s4 + (h.longl4 ? body : 0u));
+  if (shift & 1) f = swap16(f);  // RFC 1071 byte-order swap
+  const uint32_t v = (~fold16(f + h.pseudo)) & 0xffffu;
+  return (h.udp && v == 0u) ? 0xffffu : v;
+}
+
+// The wave's four byte stores (the two check fields, little-endian as the
+// reference's u16 stores): lanes with nothing to write store to the sink, so
+// the wave always issues exactly NST_TX stores.
+__device__ __forceinline__ void store_checks(const KParams& P, const DescView& dv,
+                                             const TxHdr& h, uint32_t l4v, uint32_t lane) {
+  uint8_t* const frame = reinterpret_cast<uint8_t*>(dv.abase + (uint64_t)dv.shift);
+  uint8_t* const sink = P.sink + 4u * lane;
+  const bool ip = dv.valid && h.ip_do, l4 = dv.valid && h.l4_do;
+  uint8_t* const pi = ip ? frame + h.ip_pos : sink;
+  uint8_t* const pl = l4 ? frame + h.l4_pos : sink + 2;
+  pi[0] = (uint8_t)h.ip_ck;
+  pi[1] = (uint8_t)(h.ip_ck >> 8);
+  pl[0] = (uint8_t)l4v;
+  pl[1] = (uint8_t)(l4v >> 8);
+}
+
+// ---------------------------------------------------------------------------
 // rx_kernel: every wave parses and streams its own tiles, software-pipelined:
 // while a tile's body streams, the next tile's header windows (and the
 // descriptors of the tile after it) land in LDS, so each tile starts with its
@@ -1202,7 +1332,11 @@ __device__ __forceinline__ void store_records(const KParams& P, bool valid, uint
   o[1] = src[1];
 }
 
-__global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
+// The per-wave tile loop of rx_kernel (TX = false) and tx_kernel (TX =
+// true): the same staging and body stream, different header work and stores.
+template <bool TX>
+__device__ __forceinline__ void tile_loop(const KParams& P) {
+  constexpr int NSTK = TX ? 4 : NST;  // stores per tile
   // All LDS in one __shared__ array (a second object can make hipcc wait
   // vmcnt(0) before LDS reads while LDS-DMA is in flight).
   __shared__ __attribute__((aligned(16))) uint4 smem[WAVES * WAVE_U4];
@@ -1253,22 +1387,28 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
 #pragma unroll
       for (int u = 0; u < R; ++u) issue_round(ci, J, zero, &L.ring[u][0], lane);
       if (it_ == 0) vm_wait<R>();
-      else vm_wait<R + NST>();
+      else vm_wait<R + NSTK>();
     } else {
       if (it_ == 0) vm_wait<0>();
-      else vm_wait<NST>();
+      else vm_wait<NSTK>();
     }
     STAMP(1, __builtin_amdgcn_s_memrealtime());
     STAMP(7, T);
 
     // ---- header work (one packet per lane).
+    Parsed ps;
+    TxHdr th;
+    if constexpr (TX) {
+      th = tx_header(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
+    } else {
 #ifdef OO_RX_ABL_NOPARSE
-    Parsed ps = {};
-    ps.r.reason = (uint8_t)(lds_read16(&L.hdr[0][lane]).x & 7u);
+      ps = Parsed{};
+      ps.r.reason = (uint8_t)(lds_read16(&L.hdr[0][lane]).x & 7u);
 #else
-    Parsed ps = parse_packet(P, window_of(L.hdr, lane), dv.shift, dv.len, dv.intf_i, dv.abase,
-                             dv.span);
+      ps = parse_packet(P, window_of(L.hdr, lane), dv.shift, dv.len, dv.intf_i, dv.abase,
+                        dv.span);
 #endif
+    }
     STAMP(3, __builtin_amdgcn_s_memrealtime());
 
     // ---- stage the next tile: descriptors of the tile after it into this
@@ -1303,14 +1443,20 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     }
     STAMP(4, __builtin_amdgcn_s_memrealtime());
 
-    finish(ps, lane_get(cc.bs, myslot));
-    if (P.counters != nullptr && dv.valid) lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
-    store_records(P, dv.valid, dv.idx, ps.r, lane);
+    const uint32_t body = lane_get(cc.bs, myslot);
+    if constexpr (TX) {
+      store_checks(P, dv, th, tx_l4_check(th, dv.shift, body), lane);
+    } else {
+      finish(ps, body);
+      if (P.counters != nullptr && dv.valid)
+        lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
+      store_records(P, dv.valid, dv.idx, ps.r, lane);
+    }
     STAMP(5, __builtin_amdgcn_s_memrealtime());
   }
 
   // Per-reason counts: one global atomic per reason seen by the wave.
-  if (P.counters != nullptr) {
+  if (!TX && P.counters != nullptr) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane < OO_RX_R_COUNT) {
       const uint32_t c = lds_read4(&L.cnt[lane]);
@@ -1318,6 +1464,9 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) {
     }
   }
 }
+
+__global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) { tile_loop<false>(P); }
+__global__ __launch_bounds__(WAVES * 64) void tx_kernel(KParams P) { tile_loop<true>(P); }
 
 // ---------------------------------------------------------------------------
 // rx_split: one parser wave + WS streamer waves per block.
@@ -1555,6 +1704,12 @@ extern "C" int oo_rx_blocks_per_cu(int split) {
 
 // Tile-processing waves per block: rx_kernel's waves, rx_split's streamers.
 extern "C" int oo_rx_waves_per_block(int split) { return split ? oo_rx::WS : oo_rx::WAVES; }
+
+// Launch one TX checksum fill batch on `stream` (rx_kernel's grid).
+extern "C" int oo_tx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::tx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 // Launch one batch on `stream`.
 extern "C" int oo_rx_launch(const oo_rx::KParams* P, int split, int grid, hipStream_t stream) {

@@ -167,6 +167,17 @@ class GpuRxStack:
         if rc:
             raise OSError(-rc, "oo_gpu_rx_process_dev")
 
+    def tx_fill_dev(self, frames_ptr: int, frames_bytes: int, desc_ptr: int, n: int,
+                    stream: int = 0) -> None:
+        """Enqueue the TX checksum fill (oo_pkt_calc_checksums,
+        src/lib/transport/ip/pkt_checksum.c:20-102) over HBM-resident frames,
+        in place."""
+        rc = self._lib.oo_gpu_tx_fill_dev(self._ctx, ctypes.c_void_p(frames_ptr), frames_bytes,
+                                          ctypes.c_void_p(desc_ptr), n,
+                                          ctypes.c_void_p(stream or None))
+        if rc:
+            raise OSError(-rc, "oo_gpu_tx_fill_dev")
+
     def handle_rx_batch(self, frames: np.ndarray, desc: np.ndarray):
         """Host buffers in, (results, per-reason counters) out."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)

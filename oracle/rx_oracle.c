@@ -870,3 +870,105 @@ void oo_or_rx_batch(const oo_or_tables* t, const uint8_t* frames,
   for( k = 0; k < nthreads; ++k )
     pthread_join(th[k], NULL);
 }
+
+/* ------------------------------------------------------------------ */
+/* TX checksum fill.                            */
+
+/* The fill value of an exact word sum S != 0: ip_proto_csum64_finish
+ * (checksum.c:162-174) folds with end-around carry and complements, so a
+ * sum that is a non-zero multiple of 0xffff gives 0. */
+static inline uint32_t fill_of(uint64_t s)
+{ return (~fold16(s)) & 0xffffu; }
+
+static inline void st16n(uint8_t* p, uint32_t v)
+{ p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+
+/* oo_pkt_calc_checksums (src/lib/transport/ip/pkt_checksum.c:20-102) as
+ * calc_csum_if_needed (netif_tx.c:24-40) calls it: only for TCP or UDP
+ * (ipx_hdr_protocol); the IPv4 header checksum (ef_ip_checksum,
+ * checksum.c:185-212: the 4*IHL header bytes without the check field), then
+ * the L4 check field over the rest of the frame:
+ *   UDP (ef_udp_checksum{,_ip6}, checksum.c:225-250): not for an IPv4
+ *     fragment (ci_ipx_is_frag: frag_off bits other than DF, ipvx.h:474-488);
+ *     pseudo-header + header words 0..2 + payload from udp+8; 0 -> 0xffff;
+ *   TCP (ef_tcp_checksum{,_ip6}, checksum.c:260-296): pseudo-header with
+ *     (u16)(tot_len - 4*IHL) (IPv4) or payload_len (IPv6), the 4*doff
+ *     header bytes, + 0xffff - check, payload from tcp+4*doff.
+ * The VLAN tag is parsed as on RX (ci_parse_rx_vlan).  The reference
+ * asserts the headers lie in the frame; here a frame whose headers do not
+ * fit, or with IHL < 5 or TCP doff < 5, is left untouched. */
+void oo_or_tx_fill_one(uint8_t* fr, int len)
+{
+  frame_t f = { fr, len };
+  int l3 = 14, l4, af6, ihl4 = 40;
+  unsigned proto;
+  uint64_t pseudo;
+  if( len < 14 )
+    return;
+  if( be16(f, 12) == 0x8100u )
+    l3 = 18;
+  switch( be16(f, l3 - 2) ) {
+  case 0x0800u: af6 = 0; break;
+  case 0x86ddu: af6 = 1; break;
+  default: return;
+  }
+  if( !af6 ) {
+    if( len < l3 + 20 )
+      return;
+    ihl4 = (fr[l3] & 0xf) * 4;
+    if( ihl4 < 20 || len < l3 + ihl4 )
+      return;
+    proto = fr[l3 + 9];
+  }
+  else {
+    if( len < l3 + 40 )
+      return;
+    proto = fr[l3 + 6];
+  }
+  if( proto != 6u && proto != 17u )
+    return;
+  l4 = l3 + ihl4;
+  if( !af6 )  /* ip_hdr_csum32_finish: no 0 -> 0xffff substitution */
+    st16n(fr + l3 + 10, fill_of(sum16(fr + l3, (size_t)ihl4) - rd16n(f, l3 + 10)));
+  if( proto == 17u ) {
+    uint32_t v;
+    if( !af6 && (be16(f, l3 + 6) & ~0x4000u) )
+      return;
+    if( len < l4 + 8 )
+      return;
+    pseudo = af6 ? sum16(fr + l3 + 8, 32) : ip4_addr_sum(fr + l3);
+    pseudo += 0x1100u + rd16n(f, l4 + 4);
+    v = fill_of(pseudo + sum16(fr + l4, 6) + sum16(fr + l4 + 8, (size_t)(len - l4 - 8)));
+    st16n(fr + l4 + 6, v ? v : 0xffffu);
+  }
+  else {
+    int hl4;
+    if( len < l4 + 20 )
+      return;
+    hl4 = (fr[l4 + 12] >> 4) * 4;
+    if( hl4 < 20 || len < l4 + hl4 )
+      return;
+    if( af6 ) {
+      pseudo = sum16(fr + l3 + 8, 32) + rd16n(f, l3 + 4);
+    }
+    else {
+      unsigned pl = (be16(f, l3 + 2) - (unsigned)ihl4) & 0xffffu;
+      pseudo = ip4_addr_sum(fr + l3) + (((pl & 0xffu) << 8) | (pl >> 8));
+    }
+    pseudo += 0x0600u;
+    st16n(fr + l4 + 16, fill_of(pseudo + sum16(fr + l4, (size_t)hl4) +
+                                (0xffffu - rd16n(f, l4 + 16)) +
+                                sum16(fr + l4 + hl4, (size_t)(len - l4 - hl4))));
+  }
+}
+
+void oo_or_tx_fill_batch(uint8_t* frames, uint64_t frames_bytes,
+                         const oo_gpu_pkt_desc* d, uint32_t n)
+{
+  uint32_t i;
+  for( i = 0; i < n; ++i ) {
+    uint64_t off = d[i].frame_off;
+    if( off + d[i].len <= frames_bytes )
+      oo_or_tx_fill_one(frames + off, d[i].len);
+  }
+}

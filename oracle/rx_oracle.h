@@ -57,6 +57,11 @@ int oo_or_tcp4_ok(const uint8_t* ip4, const uint8_t* tcp,
 int oo_or_tcp6_ok(const uint8_t* ip6, const uint8_t* tcp,
                   const uint8_t* pay, size_t paylen);
 
+/* TX checksum fill (pkt_checksum.c:20-102), in place. */
+void oo_or_tx_fill_one(uint8_t* frame, int len);
+void oo_or_tx_fill_batch(uint8_t* frames, uint64_t frames_bytes,
+                         const oo_gpu_pkt_desc* desc, uint32_t n);
+
 /* Hashes (src/include/onload/hash.h). */
 uint32_t oo_or_hash3(uint32_t laddr, uint32_t lport, uint32_t raddr,
                      uint32_t rport, uint32_t proto);

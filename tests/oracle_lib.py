@@ -51,6 +51,8 @@ def oracle():
             "oo_or_hash1": (_U32, [_U32] * 6),
             "oo_or_hash2": (_U32, [_U32] * 5),
             "oo_or_addr_xor": (_U32, [_P]),
+            "oo_or_tx_fill_one": (None, [_P, ctypes.c_int]),
+            "oo_or_tx_fill_batch": (None, [_P, ctypes.c_uint64, _P, _U32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -158,3 +160,22 @@ class OracleStack:
 
 def counters_of(results: np.ndarray) -> np.ndarray:
     return np.bincount(results["reason"], minlength=_abi.R_COUNT).astype(np.uint32)
+
+
+def oracle_tx_fill(buf: np.ndarray, desc: np.ndarray) -> np.ndarray:
+    """oo_pkt_calc_checksums over a batch (the oracle's restatement), on a copy."""
+    out = np.ascontiguousarray(buf).copy()
+    d = np.ascontiguousarray(desc)
+    oracle().oo_or_tx_fill_batch(out.ctypes.data, out.nbytes, d.ctypes.data, len(d))
+    return out
+
+
+def tx_golden():
+    """(frames_in, frames_out, desc) of tests/golden/ref_tx_fill.npz, packed
+    back to back."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "ref_tx_fill.npz"))
+    lens = g["lens"].astype(np.int64)
+    desc = np.zeros(len(lens), dtype=_abi.DESC_DTYPE)
+    desc["frame_off"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    desc["len"] = lens
+    return g["frames_in"].copy(), g["frames_out"].copy(), desc
