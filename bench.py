@@ -59,6 +59,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scatter", action="store_true",
                     help="N>1: also time an RCCL scatter of every shard from rank 0's GPU")
+    ap.add_argument("--tx", action="store_true",
+                    help="also time the TX checksum fill (oo_gpu_tx_fill_dev) on the same frames")
     ap.add_argument("--host-path", action="store_true",
                     help="also time pinned H2D + transform + D2H (printed to stderr)")
     args = ap.parse_args()
@@ -163,6 +165,11 @@ def main() -> None:
         host_path = time_host_path(torch, stack, buf, desc, dev)
         log(f"[rank {rank}] host path: {json.dumps(host_path)}")
 
+    tx = None
+    if args.tx:
+        tx = time_tx_fill(torch, stack, frames, d_desc, n, mean_len, sh, args.steps, args.warmup)
+        log(f"[rank {rank}] tx fill: {json.dumps(tx)}")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(filters, socks, buf, desc, args.cpu_seconds)
@@ -195,6 +202,8 @@ def main() -> None:
         }
         if host_path is not None:
             line["host_path"] = host_path
+        if tx is not None:
+            line["tx_fill"] = tx
         if scatter is not None:
             line["rccl_scatter"] = scatter
         print(json.dumps(line), flush=True)
@@ -238,6 +247,29 @@ def time_scatter(torch, dist, cfg, seed, n, rank, world, dev, my_buf, reps: int 
     s = float(np.median(times))
     return {"ms": round(s * 1e3, 3), "bytes_per_peer": slab,
             "GBps_from_root": round(slab * (world - 1) / s / 1e9, 1), "verified": bool(okt.item())}
+
+
+def time_tx_fill(torch, stack, frames, d_desc, n, mean_len, sh, steps, warmup):
+    """The TX checksum fill over the same HBM-resident frames (in place; a
+    fill of already-filled frames rewrites the same values).  Algorithmic
+    bytes: the frame read, the descriptor, the 4 check-field bytes written."""
+    for _ in range(warmup):
+        stack.tx_fill_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n, sh)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        stack.tx_fill_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n, sh)
+        e.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    bpp = mean_len + DESC_B + 4
+    gbs = n * bpp / (ms * 1e-3) / 1e9
+    return {"kernel_ms": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 1),
+            "achieved_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "bytes_per_pkt": round(bpp, 1)}
 
 
 def time_host_path(torch, stack, buf, desc, dev, reps: int = 5):
