@@ -1161,7 +1161,57 @@ struct TxHdr {
   uint32_t pseudo;  // pseudo-header words + 0xffff - old check (L4-relative)
 };
 
-__device__ __forceinline__ TxHdr tx_header(const Win& W, int shift, int len, uint64_t abase) {
+// The fixed-format TX header (16-B-aligned start, untagged IPv4 IHL 5, TCP
+// or UDP whose header fits): fields at fixed offsets from the staged cells,
+// the same decisions as tx_general.  false: another frame.
+__device__ __forceinline__ bool tx_fixed(const uint4 (&c)[HC], int shift, int len, int off0,
+                                         TxHdr& h) {
+  const uint32_t proto = c[1].y >> 24;
+  const bool tcp = proto == 6u;
+  const uint32_t doff4 = ((c[2].w >> 20) & 0xfu) * 4u;
+  bool ok = shift == 0 && off0 >= 48 && len >= 48 && (c[0].w & 0x000fffffu) == 0x00050008u &&
+            (tcp || proto == 17u);
+  ok = ok && (tcp ? (len >= 54 && doff4 >= 20u && (uint32_t)len >= 34u + doff4) : len >= 42);
+  if (!ok) return false;
+  const uint32_t frag = bswap16(c[1].y);
+  const uint32_t addrs = (c[1].z >> 16) + (c[1].w & 0xffffu) + (c[1].w >> 16) + (c[2].x & 0xffffu);
+  // IPv4 header words, bytes [14, 34) without the check field [24, 26).
+  h.ip_do = true;
+  h.ip_pos = 24;
+  h.ip_ck = (~fold16(chunk_sum_all(c[1], (c[0].w >> 16) + (c[2].x & 0xffffu)) -
+                     (c[1].z & 0xffffu))) & 0xffffu;
+  h.udp = !tcp;
+  h.l4_do = tcp || (frag & ~0x4000u) == 0u;
+  if (tcp) {
+    const uint32_t pl = (bswap16(c[1].x) - 20u) & 0xffffu;
+    h.l4_pos = 50;
+    h.pseudo = addrs + 0x0600u + bswap16(pl) + (0xffffu - (c[3].x >> 16));
+  } else {
+    h.l4_pos = 40;
+    h.pseudo = addrs + 0x1100u + (c[2].y >> 16) + (0xffffu - (c[2].z & 0xffffu));
+  }
+  // L4 window part [34, E4h), as parse_fixed.
+  const int E4 = len;
+  h.longl4 = E4 > HB;
+  const int E4h = h.longl4 ? off0 : E4;
+  uint32_t s4 = 0;
+  if (__ballot((E4h & 15) != 0) == 0) {
+#pragma unroll
+    for (int k = 2; k < HC; ++k) {
+      const uint32_t t = chunk_sum_all(c[k], 0u);
+      s4 += E4h >= 16 * k + 16 ? t : 0u;
+    }
+    s4 -= E4h >= 48 ? (c[2].x & 0xffffu) : 0u;
+  } else {
+#pragma unroll
+    for (int k = 2; k < HC; ++k)
+      if (16 * k < E4h) s4 += chunk_sum(c[k], 16 * k, 34, E4h);
+  }
+  h.s4 = s4;
+  return true;
+}
+
+__device__ __forceinline__ TxHdr tx_general(const Win& W, int shift, int len, uint64_t abase) {
   auto B = [&](int j) -> uint32_t {
     int w = shift + j;
     w = w < HB ? w : HB - 1;
@@ -1240,6 +1290,20 @@ __device__ __forceinline__ TxHdr tx_header(const Win& W, int shift, int len, uin
     if (k * 16 < hi4) s4 += chunk_sum(*reinterpret_cast<const uint4*>(W.cell(k)), k * 16, lo4, hi4);
   }
   h.s4 = cut < S4 ? 0u - s4 : s4;
+  return h;
+}
+
+__device__ __forceinline__ TxHdr tx_header(const Win& W, int shift, int len, uint64_t abase) {
+  TxHdr h;
+  bool fixed;
+  {
+    uint4 c[HC];
+    read_cells(W, c);
+    fixed = tx_fixed(c, shift, len, (int)body_off0(abase), h);
+  }
+  if (__ballot(!fixed) != 0) {
+    if (!fixed) h = tx_general(W, shift, len, abase);
+  }
   return h;
 }
 
