@@ -963,7 +963,11 @@ __device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32
 __device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint64_t zero,
                                             void* slot, uint32_t lane) {
   glds<OO_RX_BODY_AUX>(c.a, slot);
+#ifdef OO_RX_ABL_LEAN
+  c.a += 128u;
+#else
   c.a += c.rnd < c.adv ? 128u : 0u;
+#endif
   if (++c.rnd == c.R) issue_slot(c, J, c.js + 1, lane, zero);
 }
 
@@ -1003,9 +1007,14 @@ __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, u
 // their words by 0).
 __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
                                               uint32_t lane) {
+#ifdef OO_RX_ABL_LEAN
+  const bool live = true, part = false;
+  if (true) {
+#else
   const bool live = c.rnd < c.lv;
   const bool part = live && c.rnd + 1u == c.lv && c.vb != 16u;
   if (__ballot(part) == 0) {
+#endif
     const uint32_t w = live ? 0x00010001u : 0u;
     uint32_t a = dot(v.x, w, c.acc);
     uint32_t b = dot(v.y, w, 0u);
@@ -1342,8 +1351,16 @@ __device__ __forceinline__ void store_checks(const KParams& P, const DescView& d
 // one descriptor line) and NST record stores, both issued by the whole
 // wave whatever its lanes hold, so the counts are static.
 
+#ifdef OO_RX_ABL_NOHDR
+constexpr int NHS = 1;
+#else
 constexpr int NHS = HC + 1;
+#endif
+#ifdef OO_RX_ABL_NOSTORE
+constexpr int NST = 0;
+#else
 constexpr int NST = 2;
+#endif
 
 struct WaveLds {
   uint4 hdr[HC][64];            // header windows (stage_window)
@@ -1392,8 +1409,14 @@ __device__ __forceinline__ void store_records(const KParams& P, bool valid, uint
   uint4* o = valid ? reinterpret_cast<uint4*>(P.out + idx)
                    : reinterpret_cast<uint4*>(P.sink) + 2u * lane;
   const uint4* src = reinterpret_cast<const uint4*>(&r);
+#ifdef OO_RX_ST_NT
+  u32x4* const q = reinterpret_cast<u32x4*>(o);
+  __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(src), q);
+  __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(src + 1), q + 1);
+#else
   o[0] = src[0];
   o[1] = src[1];
+#endif
 }
 
 // The per-wave tile loop of rx_kernel (TX = false) and tx_kernel (TX =
@@ -1423,7 +1446,11 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   glds<0>(desc_src(P, unit_of(P, gwave + W), lane), &L.desc[1][0]);
   {
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
+#ifndef OO_RX_ABL_NOHDR  // ablation builds (timing experiments only; results are wrong)
     stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
+#else
+    (void)d0;
+#endif
   }
 
   uint32_t b = 0, it_ = 0;
@@ -1481,7 +1508,11 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     {
       const Unit nt = unit_of(P, gwave + (it_ + 1u) * W);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
+#ifndef OO_RX_ABL_NOHDR
       stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
+#else
+      (void)dn;
+#endif
     }
 
     // ---- body stream (T is a multiple of R), two pieces per step.  Pieces
@@ -1514,7 +1545,9 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       finish(ps, body);
       if (P.counters != nullptr && dv.valid)
         lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
+#ifndef OO_RX_ABL_NOSTORE
       store_records(P, dv.valid, dv.idx, ps.r, lane);
+#endif
     }
     STAMP(5, __builtin_amdgcn_s_memrealtime());
   }
@@ -1541,8 +1574,9 @@ __global__ __launch_bounds__(WAVES * 64) void tx_kernel(KParams P) { tile_loop<t
 // body sums the streamers left in LDS before the barrier that ends phase
 // k-1.  A streamer's ring runs on across tiles and barriers: once its tile's
 // pieces are all issued it issues the next tile's (its descriptors are
-// fetched two phases ahead), so the stream never drains.  The parser uses
-// no LDS-DMA: its loads and LDS accesses are ordinary ones.
+// fetched three phases ahead), so the stream never drains.  The parser
+// stages each tile's header windows by LDS-DMA and waits for them
+// (vmcnt(0)) in its own wave, away from the streamers' counted waits.
 
 struct StreamerLds {
   uint4 ring[SR][64];    // body ring
