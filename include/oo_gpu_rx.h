@@ -222,10 +222,6 @@ int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* ctx, const void* d_frames,
                           oo_gpu_rx_result* d_out,
                           oo_gpu_rx_counters* d_counters, void* stream);
 
-/* Host-memory batch (the NIC ring -> socket path): copies frames and
- * descriptors host->device, runs the transform, copies results (and the
- * per-reason deltas, if `delta` is not NULL) back, and waits.  Frame bytes
- * and n must fit the staging sizes given at open.  Returns n or -errno. */
 /* TX checksum fill on HBM-resident frames, in place, asynchronous on
  * `stream`: for each descriptor, oo_pkt_calc_checksums
  * (src/lib/transport/ip/pkt_checksum.c:20-102) as calc_csum_if_needed
@@ -241,6 +237,47 @@ int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* ctx, const void* d_frames,
 int oo_gpu_tx_fill_dev(oo_gpu_rx_ctx* ctx, void* d_frames, uint64_t frames_bytes,
                        const oo_gpu_pkt_desc* d_desc, uint32_t n, void* stream);
 
+/* AF_XDP RX ring entry (struct xdp_desc, <linux/if_xdp.h>). */
+typedef struct oo_gpu_xdp_desc {
+  uint64_t addr;     /* UMEM offset of the frame's first byte */
+  uint32_t len;      /* frame length */
+  uint32_t options;  /* not read */
+} oo_gpu_xdp_desc;
+
+/* The transform straight off an AF_XDP RX ring, asynchronous on `stream`:
+ * n entries from consumer index `cons`, entry i at
+ * d_ring[(cons + i) & ring_mask] (ring_mask + 1 a power of two, n at most
+ * that), record i to d_out[i].  As efxdp_ef_eventq_poll
+ * (src/lib/ciul/efxdp_vi.c:309-358) with netif_event.c:1715-1736 turns an
+ * entry into a packet: buffer addr / 2048, frame at offset addr & 2047 --
+ * UMEM + addr -- of length len as ef_event's 16-bit rx.len (ef_vi.h:154)
+ * carries it, on the ring's interface intf_i.  d_umem / umem_bytes play the
+ * frame buffer's part (an entry outside it is an empty frame).  The ring may
+ * be device memory or host memory the device can read (hipHostRegister).
+ * Returns 0 or -errno. */
+int oo_gpu_rx_xdp_dev(oo_gpu_rx_ctx* ctx, const void* d_umem, uint64_t umem_bytes,
+                      const oo_gpu_xdp_desc* d_ring, uint32_t ring_mask,
+                      uint32_t cons, uint32_t n, int intf_i,
+                      oo_gpu_rx_result* d_out, oo_gpu_rx_counters* d_counters,
+                      void* stream);
+
+/* One batched poll of an AF_XDP RX ring (efxdp_ef_eventq_poll's RX branch,
+ * efxdp_vi.c:316-356, for up to max_n entries instead of evs_len events):
+ * reads *consumer and *producer (host words), runs oo_gpu_rx_xdp_dev over
+ * the min(producer - consumer, max_n) entries, waits for the stream, then
+ * publishes the consumer index (the reference's ci_mb() and store,
+ * :352-355) -- only after the device has read the entries.
+ * Returns the number of entries consumed or -errno. */
+int oo_gpu_rx_xdp_poll(oo_gpu_rx_ctx* ctx, const void* d_umem, uint64_t umem_bytes,
+                       const oo_gpu_xdp_desc* d_ring, uint32_t ring_mask,
+                       volatile uint32_t* consumer, const volatile uint32_t* producer,
+                       uint32_t max_n, int intf_i, oo_gpu_rx_result* d_out,
+                       oo_gpu_rx_counters* d_counters, void* stream);
+
+/* Host-memory batch (the NIC ring -> socket path): copies frames and
+ * descriptors host->device, runs the transform, copies results (and the
+ * per-reason deltas, if `delta` is not NULL) back, and waits.  Frame bytes
+ * and n must fit the staging sizes given at open.  Returns n or -errno. */
 int oo_gpu_rx_batch(oo_gpu_rx_ctx* ctx, const void* frames,
                     uint64_t frames_bytes, const oo_gpu_pkt_desc* desc,
                     uint32_t n, oo_gpu_rx_result* out,

@@ -40,7 +40,10 @@ RESULT_DTYPE = np.dtype([
     ("vlan", "<u2"), ("l4_off", "<u2"), ("ip_paylen", "<u2"), ("sport_be", "<u2"),
     ("dport_be", "<u2"), ("nmatch", "<u2"), ("saddr_be", "<u4"), ("daddr_be", "<u4"),
     ("sock", "<i4"), ("hash3", "<u4")])
+# struct xdp_desc (<linux/if_xdp.h>), an AF_XDP RX ring entry.
+XDP_DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
 assert DESC_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 32
+assert XDP_DESC_DTYPE.itemsize == 16
 
 
 class Sock(ctypes.Structure):
@@ -89,6 +92,10 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_sync_tables": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_process_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _P]),
     "oo_gpu_tx_fill_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P]),
+    "oo_gpu_rx_xdp_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _U32, _U32, ctypes.c_int,
+                                         _P, _P, _P]),
+    "oo_gpu_rx_xdp_poll": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _U32, ctypes.c_int,
+                                          _P, _P, _P]),
     "oo_gpu_rx_batch": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P]),
     "oo_gpu_rx_reason_str": (ctypes.c_char_p, [ctypes.c_int]),
 }

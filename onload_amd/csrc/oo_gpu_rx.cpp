@@ -577,12 +577,22 @@ int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
 // tx: the TX checksum fill (tx_kernel) instead of the RX transform.
 static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
                   const oo_gpu_pkt_desc* d_desc, uint32_t n, oo_gpu_rx_result* d_out,
-                  uint32_t* d_ctr, hipStream_t s, bool tx = false) {
+                  uint32_t* d_ctr, hipStream_t s, bool tx = false,
+                  const oo_gpu_xdp_desc* d_ring = nullptr, uint32_t ring_mask = 0,
+                  uint32_t cons = 0, int intf_i = 0) {
   KParams P;
   memset(&P, 0, sizeof(P));
   P.frames = static_cast<const uint8_t*>(d_frames);
   P.frames_bytes = frames_bytes;
   P.desc = d_desc;
+  P.ring_mask = ~0u;
+  if (d_ring != nullptr) {  // both entry layouts are 16 B, offset first
+    P.desc = reinterpret_cast<const oo_gpu_pkt_desc*>(d_ring);
+    P.ring_mask = ring_mask;
+    P.ring_cons = cons;
+    P.xdp = 1;
+    P.xdp_intf = intf_i;
+  }
   P.out = d_out;
   P.counters = d_ctr;
   P.n = n;
@@ -636,6 +646,46 @@ int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frame
   if (rc) return rc;
   return launch(c, d_frames, frames_bytes, d_desc, n, d_out,
                 reinterpret_cast<uint32_t*>(d_counters), s);
+}
+
+int oo_gpu_rx_xdp_dev(oo_gpu_rx_ctx* c, const void* d_umem, uint64_t umem_bytes,
+                      const oo_gpu_xdp_desc* d_ring, uint32_t ring_mask, uint32_t cons,
+                      uint32_t n, int intf_i, oo_gpu_rx_result* d_out,
+                      oo_gpu_rx_counters* d_counters, void* stream) {
+  static_assert(sizeof(oo_gpu_xdp_desc) == 16 && sizeof(oo_gpu_pkt_desc) == 16,
+                "16-B ring entries");
+  if (c == nullptr || (ring_mask & (ring_mask + 1u)) != 0 || ring_mask == ~0u ||
+      (uint64_t)n > (uint64_t)ring_mask + 1u ||
+      (n > 0 && (d_umem == nullptr || d_ring == nullptr || d_out == nullptr)))
+    return -EINVAL;
+  if (c->device < 0) return -ENODEV;
+  if (n == 0) return 0;
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = sync_tables(c, s);
+  if (rc) return rc;
+  return launch(c, d_umem, umem_bytes, nullptr, n, d_out,
+                reinterpret_cast<uint32_t*>(d_counters), s, false, d_ring, ring_mask, cons,
+                intf_i);
+}
+
+int oo_gpu_rx_xdp_poll(oo_gpu_rx_ctx* c, const void* d_umem, uint64_t umem_bytes,
+                       const oo_gpu_xdp_desc* d_ring, uint32_t ring_mask,
+                       volatile uint32_t* consumer, const volatile uint32_t* producer,
+                       uint32_t max_n, int intf_i, oo_gpu_rx_result* d_out,
+                       oo_gpu_rx_counters* d_counters, void* stream) {
+  if (consumer == nullptr || producer == nullptr) return -EINVAL;
+  const uint32_t cons = *consumer;
+  const uint32_t prod = *producer;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // entries are read after the producer index
+  const uint32_t n = std::min<uint32_t>(prod - cons, max_n);
+  int rc = oo_gpu_rx_xdp_dev(c, d_umem, umem_bytes, d_ring, ring_mask, cons, n, intf_i, d_out,
+                             d_counters, stream);
+  if (rc != 0 || n == 0) return rc;
+  if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return -EIO;
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);  // the reference's ci_mb() before the store
+  *consumer = cons + n;
+  return (int)n;
 }
 
 int oo_gpu_tx_fill_dev(oo_gpu_rx_ctx* c, void* d_frames, uint64_t frames_bytes,

@@ -74,7 +74,11 @@ constexpr uint32_t ZERO_LINES = 4096;
 struct KParams {
   const uint8_t* frames;
   uint64_t frames_bytes;
-  const oo_gpu_pkt_desc* desc;
+  const oo_gpu_pkt_desc* desc;  // or struct xdp_desc[ring_mask + 1] (xdp)
+  uint32_t ring_mask;    // descriptor i is desc[(ring_cons + i) & ring_mask]
+  uint32_t ring_cons;    // (~0u and 0 for a plain descriptor array)
+  uint32_t xdp;          // 1: AF_XDP ring entries {u64 addr; u32 len; u32 options}
+  int32_t xdp_intf;      // the ring's interface (xdp)
   oo_gpu_rx_result* out;
   uint32_t* counters;  // OO_RX_R_COUNT u32, may be null
   uint32_t n;

@@ -1084,9 +1084,13 @@ __device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, 
   DescView v;
   v.idx = t.first + lane;
   v.valid = lane < t.cnt;
+  // Both layouts: {u64 offset, 16-bit length, ...}.  An AF_XDP entry's u32
+  // len is carried in ef_event's 16-bit rx.len (ef_vi.h:154,
+  // efxdp_vi.c:349), and its frame starts at UMEM + addr: buffer addr / 2048
+  // at offset addr & 2047 (efxdp_vi.c:337-348, netif_event.c:1723-1727).
   const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
   int len = (int)(d.z & 0xffffu);
-  v.intf_i = (int)(int16_t)(d.z >> 16);
+  v.intf_i = P.xdp ? P.xdp_intf : (int)(int16_t)(d.z >> 16);
   const bool inb = v.valid && off + (uint64_t)len <= P.frames_bytes;
   if (!inb) len = 0;  // a descriptor outside the buffer is an empty frame
   const uint64_t base = reinterpret_cast<uint64_t>(P.frames) + (inb ? off : 0);
@@ -1099,9 +1103,11 @@ __device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, 
 
 // Where lane `lane` of unit t loads its descriptor from (lanes without a
 // packet: some other in-bounds entry).
+__device__ __forceinline__ uint64_t desc_at(const KParams& P, uint32_t i) {
+  return reinterpret_cast<uint64_t>(P.desc) + (uint64_t)((P.ring_cons + i) & P.ring_mask) * 16;
+}
 __device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, uint32_t lane) {
-  return reinterpret_cast<uint64_t>(P.desc) +
-         (uint64_t)(lane < t.cnt ? t.first + lane : lane % P.n) * 16;
+  return desc_at(P, lane < t.cnt ? t.first + lane : lane % P.n);
 }
 
 // Per-reason counters: one global atomic per distinct reason in the wave
@@ -1600,7 +1606,7 @@ __device__ __forceinline__ void block_barrier() {
 __device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (*hdr)[64], const Unit& t,
                                              uint32_t lane) {
   uint4 d = make_uint4(0, 0, 0, 0);
-  if (lane < t.cnt) d = *reinterpret_cast<const uint4*>(P.desc + t.first + lane);
+  if (lane < t.cnt) d = *reinterpret_cast<const uint4*>(desc_at(P, t.first + lane));
   const DescView dv = desc_view(P, d, t, lane);
   stage_window(dv, zero_line(P, t, lane), hdr, lane);
   vm_wait<0>();

@@ -178,6 +178,38 @@ class GpuRxStack:
         if rc:
             raise OSError(-rc, "oo_gpu_tx_fill_dev")
 
+    def xdp_dev(self, umem_ptr: int, umem_bytes: int, ring_ptr: int, ring_mask: int,
+                cons: int, n: int, intf_i: int, out_ptr: int, counters_ptr: int = 0,
+                stream: int = 0) -> None:
+        """Enqueue the transform of n AF_XDP RX ring entries from consumer
+        index cons (efxdp_ef_eventq_poll, src/lib/ciul/efxdp_vi.c:309-358);
+        record i for entry (cons + i) & ring_mask."""
+        rc = self._lib.oo_gpu_rx_xdp_dev(self._ctx, ctypes.c_void_p(umem_ptr), umem_bytes,
+                                         ctypes.c_void_p(ring_ptr), ring_mask, cons, n,
+                                         intf_i, ctypes.c_void_p(out_ptr),
+                                         ctypes.c_void_p(counters_ptr or None),
+                                         ctypes.c_void_p(stream or None))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_xdp_dev")
+
+    def xdp_poll(self, umem_ptr: int, umem_bytes: int, ring_ptr: int, ring_mask: int,
+                 consumer: np.ndarray, producer: np.ndarray, max_n: int, intf_i: int,
+                 out_ptr: int, counters_ptr: int = 0, stream: int = 0) -> int:
+        """One batched ring poll: consumes min(producer - consumer, max_n)
+        entries, advances consumer[0] after the device has read them, returns
+        the count."""
+        assert consumer.dtype == np.uint32 and producer.dtype == np.uint32
+        rc = self._lib.oo_gpu_rx_xdp_poll(self._ctx, ctypes.c_void_p(umem_ptr), umem_bytes,
+                                          ctypes.c_void_p(ring_ptr), ring_mask,
+                                          consumer.ctypes.data_as(ctypes.c_void_p),
+                                          producer.ctypes.data_as(ctypes.c_void_p), max_n,
+                                          intf_i, ctypes.c_void_p(out_ptr),
+                                          ctypes.c_void_p(counters_ptr or None),
+                                          ctypes.c_void_p(stream or None))
+        if rc < 0:
+            raise OSError(-rc, "oo_gpu_rx_xdp_poll")
+        return rc
+
     def handle_rx_batch(self, frames: np.ndarray, desc: np.ndarray):
         """Host buffers in, (results, per-reason counters) out."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)

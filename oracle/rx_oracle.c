@@ -962,6 +962,32 @@ void oo_or_tx_fill_one(uint8_t* fr, int len)
   }
 }
 
+/* efxdp_ef_eventq_poll's RX branch (src/lib/ciul/efxdp_vi.c:316-356) and
+ * the event -> packet step of ci_netif_poll_evq (netif_event.c:1715-1736),
+ * for n entries from consumer index cons: entry (cons + i) & mask gives
+ * rq_id = addr / 2048, ofs = addr & 2047 (the frame at UMEM + addr, its
+ * buffer being UMEM + rq_id * 2048), rx.len = the low 16 bits of len
+ * (ef_event's 16-bit field, ef_vi.h:154), then the per-packet path on the
+ * ring's interface.  An entry outside the UMEM is an empty frame (the
+ * batch boundary's rule, not the reference's: it would read wild memory). */
+void oo_or_xdp_batch(const oo_or_tables* t, const uint8_t* umem,
+                     uint64_t umem_bytes, const oo_gpu_xdp_desc* ring,
+                     uint32_t mask, uint32_t cons, uint32_t n, int intf_i,
+                     oo_gpu_rx_result* out)
+{
+  uint32_t i;
+  for( i = 0; i < n; ++i ) {
+    const oo_gpu_xdp_desc* e = &ring[(cons + i) & mask];
+    const uint64_t rq_id = e->addr / 2048u, ofs = e->addr & 2047u;
+    const int len = (int)(e->len & 0xffffu);
+    const uint64_t at = rq_id * 2048u + ofs;
+    if( at + (uint64_t)len <= umem_bytes )
+      oo_or_rx_one(t, umem + at, len, intf_i, &out[i]);
+    else
+      oo_or_rx_one(t, umem, 0, intf_i, &out[i]);
+  }
+}
+
 void oo_or_tx_fill_batch(uint8_t* frames, uint64_t frames_bytes,
                          const oo_gpu_pkt_desc* d, uint32_t n)
 {

@@ -44,6 +44,12 @@ void oo_or_rx_batch(const oo_or_tables* t, const uint8_t* frames,
                     const oo_gpu_pkt_desc* desc, uint32_t n,
                     oo_gpu_rx_result* out, int nthreads);
 
+/* The batch straight off an AF_XDP RX ring (efxdp_vi.c:316-356). */
+void oo_or_xdp_batch(const oo_or_tables* t, const uint8_t* umem,
+                     uint64_t umem_bytes, const oo_gpu_xdp_desc* ring,
+                     uint32_t mask, uint32_t cons, uint32_t n, int intf_i,
+                     oo_gpu_rx_result* out);
+
 /* Checksum verifiers with the reference's argument shapes
  * (checksum.c:298-351, netif_event.c:80-94) for pinning against the
  * compiled reference. */

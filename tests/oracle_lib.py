@@ -53,6 +53,8 @@ def oracle():
             "oo_or_addr_xor": (_U32, [_P]),
             "oo_or_tx_fill_one": (None, [_P, ctypes.c_int]),
             "oo_or_tx_fill_batch": (None, [_P, ctypes.c_uint64, _P, _U32]),
+            "oo_or_xdp_batch": (None, [_P, _P, ctypes.c_uint64, _P, _U32, _U32, _U32,
+                                       ctypes.c_int, _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -155,6 +157,16 @@ class OracleStack:
         out = np.zeros(len(desc), dtype=_abi.RESULT_DTYPE)
         self._lib.oo_or_rx_batch(self._t, frames.ctypes.data, desc.ctypes.data, len(desc),
                                  out.ctypes.data, nthreads)
+        return out
+
+
+    def handle_xdp_batch(self, umem: np.ndarray, ring: np.ndarray, mask: int, cons: int,
+                         n: int, intf_i: int):
+        umem = np.ascontiguousarray(umem, dtype=np.uint8)
+        ring = np.ascontiguousarray(ring, dtype=_abi.XDP_DESC_DTYPE)
+        out = np.zeros(n, dtype=_abi.RESULT_DTYPE)
+        self._lib.oo_or_xdp_batch(self._t, umem.ctypes.data, umem.nbytes, ring.ctypes.data,
+                                  mask, cons, n, intf_i, out.ctypes.data)
         return out
 
 
