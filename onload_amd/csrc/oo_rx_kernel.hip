@@ -650,6 +650,73 @@ __device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int
   return true;
 }
 
+// The fixed-format IPv6 header: 16-B-aligned start, untagged Ethernet, IPv6
+// with TCP or UDP as the next header (netif_event.c:1060-1076: no extension
+// header walk) whose length fields pass the gates.  L3 at window byte 14,
+// addresses at 22 and 38, L4 at 54.  The same decisions as parse_general for
+// these frames; false (h untouched) for every other frame.
+__device__ __forceinline__ bool parse_fixed6(const uint4 (&c)[HC], int shift, int len, int off0,
+                                             Hdr& h) {
+  const int ip_paylen = (int)bswap16(c[1].x >> 16);
+  const uint32_t proto = c[1].y & 0xffu;
+  const uint32_t udp_len = bswap16(c[3].z >> 16);
+  const int hlen = (int)(((c[4].x >> 16) & 0xf0u) >> 2);
+  const bool tcp = proto == 6u;
+  bool ok = shift == 0 && off0 >= 64 && (c[0].w & 0xffffu) == 0xdd86u && ip_paylen > 0 &&
+            len >= 54 + ip_paylen;
+  ok = ok && (tcp ? (ip_paylen >= 20 && hlen >= 20 && ip_paylen >= hlen)
+                  : (proto == 17u && ip_paylen >= 8 && udp_len >= 8u && udp_len <= (uint32_t)ip_paylen));
+  if (!ok) return false;
+  const int E4 = 54 + (tcp ? ip_paylen : (int)udp_len);
+  // Pseudo header (checksum.c:215-223): the 16 address words [22, 54), then
+  // payload_len (TCP) or the UDP length field, and the protocol.
+  uint32_t pseudo = (c[1].y >> 16) + (c[1].z & 0xffffu) + (c[1].z >> 16) + (c[1].w & 0xffffu) +
+                    (c[1].w >> 16) + (c[3].x & 0xffffu) + (c[3].x >> 16) + (c[3].y & 0xffffu);
+  pseudo = chunk_sum_all(c[2], pseudo) +
+           (tcp ? (c[1].x >> 16) + 0x0600u : (c[3].z >> 16) + 0x1100u);
+  // The L4 words in the window, [54, E4h).
+  const int E4h = E4 > HB ? off0 : E4;
+  uint32_t s4 = 0;
+  if (__ballot((E4h & 15) != 0) == 0) {  // the region ends on a cell edge (wave-uniform test)
+#pragma unroll
+    for (int k = 3; k < HC; ++k) {
+      const uint32_t t = chunk_sum_all(c[k], 0u);
+      s4 += E4h >= 16 * k + 16 ? t : 0u;
+    }
+    s4 -= E4h >= 64 ? (c[3].x & 0xffffu) + (c[3].x >> 16) + (c[3].y & 0xffffu) : 0u;  // [48, 54)
+  } else {
+#pragma unroll
+    for (int k = 3; k < HC; ++k)
+      if (16 * k < E4h) s4 += chunk_sum(c[k], 16 * k, 54, E4h);
+  }
+  const bool longl4 = E4 > HB;
+  h.reason = (!longl4 && fold16(fold16(s4) + pseudo) != 0xffffu)
+                 ? (tcp ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM) : PENDING;
+  h.late = PENDING;
+  h.flags = OO_RX_F_IP6;
+  h.vlan = 0;
+  h.proto = proto;
+  h.ip_paylen = (uint32_t)ip_paylen;
+  h.l4 = 54;
+  h.l3ok = true;
+  h.is6 = true;
+  h.longl4 = longl4;
+  h.sport = c[3].y >> 16;
+  h.dport = c[3].z & 0xffffu;
+  h.sa[0] = (c[1].y >> 16) | (c[1].z << 16);
+  h.sa[1] = (c[1].z >> 16) | (c[1].w << 16);
+  h.sa[2] = (c[1].w >> 16) | (c[2].x << 16);
+  h.sa[3] = (c[2].x >> 16) | (c[2].y << 16);
+  h.da[0] = (c[2].y >> 16) | (c[2].z << 16);
+  h.da[1] = (c[2].z >> 16) | (c[2].w << 16);
+  h.da[2] = (c[2].w >> 16) | (c[3].x << 16);
+  h.da[3] = (c[3].x >> 16) | (c[3].y << 16);
+  h.s4 = s4;
+  h.pseudo = pseudo;
+  h.E4 = E4;
+  return true;
+}
+
 // The staged window of this lane's packet in registers (one LDS wait).
 __device__ __forceinline__ void read_cells(const Win& W, uint4 (&c)[HC]) {
   static_assert(HC == 8, "eight window cells");
@@ -679,6 +746,11 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, i
     uint4 c[HC];
     read_cells(W, c);
     fixed = parse_fixed(c, shift, len, off0, h);
+    if (__ballot(!fixed && (c[0].w & 0xffffu) == 0xdd86u) != 0) {
+      bool f6 = false;
+      if (!fixed) f6 = parse_fixed6(c, shift, len, off0, h);
+      fixed = fixed || f6;
+    }
   }
   if (__ballot(!fixed) != 0) {
     if (!fixed) h = parse_general(W, shift, len, off0);
