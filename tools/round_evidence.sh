@@ -22,7 +22,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
 rc=$?
 tail -3 "$OUT/gpu_tests.log"
 [ $rc -ne 0 ] && { echo "gpu tests failed rc=$rc"; exit $rc; }
-step bench2 timeout -k 10 300 sh -c "python bench.py --config 2 --steps 50 --warmup 5 --host-path > $OUT/bench_config2.json 2> $OUT/bench_config2.err"
+step bench2 timeout -k 10 300 sh -c "python bench.py --config 2 --steps 50 --warmup 5 --host-path --tx --xdp > $OUT/bench_config2.json 2> $OUT/bench_config2.err"
 cat "$OUT/bench_config2.json"
 for c in 3 4 5; do
   step bench$c timeout -k 10 300 sh -c "python bench.py --config $c --steps 20 --warmup 3 --cpu-seconds 5 > $OUT/bench_config$c.json 2> $OUT/bench_config$c.err"
