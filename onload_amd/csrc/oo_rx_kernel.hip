@@ -1480,21 +1480,29 @@ __device__ __forceinline__ void vm_wait_n(int n) {
   }
 }
 
-// The record of every lane: lanes without a packet write the sink, so the
-// wave always issues exactly NST stores.
-__device__ __forceinline__ void store_records(const KParams& P, bool valid, uint32_t idx,
+// The tile's records (packet p's in lane p): the wave writes them as two
+// contiguous 1-KiB runs, store u taking records 32u .. 32u + 31 with lane L
+// writing half L & 1 of record 32u + L / 2 -- whole lines per instruction,
+// not 16 B at a 32-B stride.  Records past the tile's count go to the sink,
+// so the wave always issues exactly NST stores.  All lanes active.
+__device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
                                               const oo_gpu_rx_result& r, uint32_t lane) {
-  uint4* o = valid ? reinterpret_cast<uint4*>(P.out + idx)
-                   : reinterpret_cast<uint4*>(P.sink) + 2u * lane;
-  const uint4* src = reinterpret_cast<const uint4*>(&r);
-#ifdef OO_RX_ST_NT
-  u32x4* const q = reinterpret_cast<u32x4*>(o);
-  __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(src), q);
-  __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(src + 1), q + 1);
-#else
-  o[0] = src[0];
-  o[1] = src[1];
-#endif
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
+  const bool hi = (lane & 1u) != 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 2; ++u) {
+    const uint32_t q = 32u * u + (lane >> 1);
+    uint4 v;
+    uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t a = lane_get(w[d], q), b = lane_get(w[4 + d], q);
+      vw[d] = hi ? b : a;
+    }
+    uint4* o = q < t.cnt ? reinterpret_cast<uint4*>(P.out + t.first + q)
+                         : reinterpret_cast<uint4*>(P.sink) + 2u * q;
+    o[hi ? 1 : 0] = v;
+  }
 }
 
 // The per-wave tile loop of rx_kernel (TX = false) and tx_kernel (TX =
@@ -1624,7 +1632,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       if (P.counters != nullptr && dv.valid)
         lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
 #ifndef OO_RX_ABL_NOSTORE
-      store_records(P, dv.valid, dv.idx, ps.r, lane);
+      store_records(P, tile, ps.r, lane);
 #endif
     }
     STAMP(5, __builtin_amdgcn_s_memrealtime());
@@ -1640,7 +1648,9 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   }
 }
 
-__global__ __launch_bounds__(WAVES * 64) void rx_kernel(KParams P) { tile_loop<false>(P); }
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void rx_kernel(KParams P) {
+  tile_loop<false>(P);
+}
 __global__ __launch_bounds__(WAVES * 64) void tx_kernel(KParams P) { tile_loop<true>(P); }
 
 // ---------------------------------------------------------------------------
