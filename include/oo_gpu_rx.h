@@ -84,6 +84,10 @@ enum {
 #define OO_RX_F_MCAST   0x08u  /* daddr multicast/broadcast: host must keep
                                   delivering to every match (udp_rx.c:148-203)     */
 #define OO_RX_F_MULTI   0x10u  /* nmatch > 1 in the deciding stage               */
+#define OO_RX_F_TSO     0x20u  /* TCP header in the timestamp-option fast layout
+                                  (doff 8, options NOP NOP TS 10: tcp_rx.c:4537-4543,
+                                  CI_TCP_TSO_WORD ip_shared_types.h:2742); the host
+                                  reads TSval/TSecr at l4_off + 24 / + 28         */
 
 /* One frame in the batch.  16 bytes. */
 typedef struct oo_gpu_pkt_desc {

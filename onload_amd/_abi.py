@@ -30,7 +30,7 @@ REASON_NAMES = {
     21: "PROTO_OTHER", 22: "TCP_SHORT", 23: "TCP_CSUM", 24: "UDP_SHORT", 25: "UDP_CSUM",
 }
 
-F_IP6, F_VLAN, F_CSUM_OK, F_MCAST, F_MULTI = 0x01, 0x02, 0x04, 0x08, 0x10
+F_IP6, F_VLAN, F_CSUM_OK, F_MCAST, F_MULTI, F_TSO = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 SOCK_CONNECTED, SOCK_BIND2DEV = 0x1, 0x2
 
 DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("len", "<u2"), ("intf_i", "<i2"),

@@ -523,6 +523,9 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
       reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
   }
 
+  // The TCP timestamp-option fast layout (tcp_rx.c:4537-4543).
+  if (reason == PENDING && proto == 6u && B(l4 + 12) == 0x80u && N32(l4 + 20) == 0x0a080101u)
+    h.flags |= OO_RX_F_TSO;
   h.reason = reason;
   h.proto = proto;
   h.ip_paylen = (uint32_t)ip_paylen;
@@ -630,7 +633,9 @@ __device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int
     reason = tcp ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
   h.reason = reason;
   h.late = (tcp && frag != 0x4000u && frag != 0u) ? OO_RX_R_TCP_SCATTERED : PENDING;
-  h.flags = 0;
+  // The TCP timestamp-option fast layout (tcp_rx.c:4537-4543): bytes 46, 54-57.
+  h.flags = (reason == PENDING && tcp && ((c[2].w >> 16) & 0xffu) == 0x80u &&
+             ((c[3].y >> 16) | (c[3].z << 16)) == 0x0a080101u) ? OO_RX_F_TSO : 0u;
   h.vlan = 0;
   h.proto = proto;
   h.ip_paylen = (uint32_t)ip_paylen;
@@ -693,7 +698,10 @@ __device__ __forceinline__ bool parse_fixed6(const uint4 (&c)[HC], int shift, in
   h.reason = (!longl4 && fold16(fold16(s4) + pseudo) != 0xffffu)
                  ? (tcp ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM) : PENDING;
   h.late = PENDING;
-  h.flags = OO_RX_F_IP6;
+  // The TCP timestamp-option fast layout (tcp_rx.c:4537-4543): bytes 66, 74-77.
+  h.flags = OO_RX_F_IP6 |
+            ((h.reason == PENDING && tcp && ((c[4].x >> 16) & 0xffu) == 0x80u &&
+              ((c[4].z >> 16) | (c[4].w << 16)) == 0x0a080101u) ? OO_RX_F_TSO : 0u);
   h.vlan = 0;
   h.proto = proto;
   h.ip_paylen = (uint32_t)ip_paylen;

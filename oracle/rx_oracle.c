@@ -751,6 +751,12 @@ void oo_or_rx_one(const oo_or_tables* t, const uint8_t* frame, int len,
   /* Handled: __handle_rx_pkt -> ci_parse_rx_vlan -> handle_rx_pkt
    * (netif_event.c:688-697, 250-451). */
   r->flags |= OO_RX_F_CSUM_OK;
+  /* The TCP timestamp-option fast layout that ci_tcp_rx_deliver_to_conn
+   * tests before its full option parser (tcp_rx.c:4537-4543): the header
+   * length byte exactly (20 + 12) << 2, the first options word
+   * CI_TCP_TSO_WORD = NOP NOP TIMESTAMP 10 (ip_shared_types.h:2742). */
+  if( proto == 6 && rd8(f, l4 + 12) == 0x80u && rd32n(f, l4 + 20) == 0x0a080101u )
+    r->flags |= OO_RX_F_TSO;
   r->l4_off = (uint16_t)l4;
   r->sport_be = (uint16_t)rd16n(f, l4);
   r->dport_be = (uint16_t)rd16n(f, l4 + 2);

@@ -176,6 +176,13 @@ def _u4(sp, dp, pay, **kw):
                         ulen=kw.pop("ulen", None), csum=kw.pop("ucsum", "ok")), **kw), 0x0800)
 
 
+_TSO = b"\x01\x01\x08\x0a" + struct.pack("!II", 0x11223344, 0x55667788)
+# (doff, options): the fast layout first, then near misses.
+TSO_VARIANTS = ((8, _TSO), (9, _TSO + b"\x01" * 4), (7, _TSO[:8]),
+                (8, b"\x01\x01\x08\x0b" + _TSO[4:]), (8, b"\x08\x0a" + _TSO[4:] + b"\x01\x01"),
+                (8, b"\x01\x01\x05\x0a" + _TSO[4:]))
+
+
 def edge_frames(seed: int = 1234) -> list[tuple[bytes, int]]:
     """List of (frame, intf_i)."""
     rnd = random.Random(seed)
@@ -310,6 +317,20 @@ def edge_frames(seed: int = 1234) -> list[tuple[bytes, int]]:
         k = rnd.randrange(12, 14 + 60)
         b[k] ^= 1 << rnd.randrange(8)
         add(bytes(b))
+    # TCP timestamp-option fast layout (tcp_rx.c:4537-4543): doff 8 with the
+    # options word NOP NOP TS 10; near misses (doff 7/9, other option words),
+    # a bad checksum, VLAN, IPv6, frames long enough to need the body.
+    for doff, opts in TSO_VARIANTS:
+        for n in (0, 13, 1200):
+            add(eth(ipv4(PEER4, L4A, 6, tcp(4, PEER4, L4A, 40000, 80, pay(n), doff=doff,
+                                            options=opts)), 0x0800))
+            add(eth(ipv6(PEER6, L6A, 6, tcp(6, PEER6, L6A, 41000, 443, pay(n), doff=doff,
+                                            options=opts)), 0x86DD))
+        add(eth(ipv4(PEER4, L4A, 6, tcp(4, PEER4, L4A, 40000, 80, pay(5), doff=doff,
+                                        options=opts)), 0x0800, vlan=7))
+        for n in (5, 1500):
+            add(eth(ipv4(PEER4, L4A, 6, tcp(4, PEER4, L4A, 40000, 80, pay(n), doff=doff,
+                                            options=opts, csum="bad")), 0x0800))
     return out
 
 

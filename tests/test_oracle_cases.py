@@ -58,3 +58,25 @@ def test_batch_threads_agree():
     # every reason the corpus is meant to reach is reached
     reasons = set(np.unique(a["reason"]).tolist())
     assert {0, 1, 2, 3, 4, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25} <= reasons, reasons
+
+
+def test_tcp_timestamp_fast_layout_flag():
+    """OO_RX_F_TSO exactly for TCP headers of length 32 whose first options
+    word is NOP NOP TIMESTAMP 10 (tcp_rx.c:4537-4543), checksum passed."""
+    from frames import L4A, L6A, PEER4, PEER6, TSO_VARIANTS, edge_world, eth, ipv4, ipv6, tcp
+    from onload_amd import _abi
+    st = OracleStack()
+    install(st, edge_world())
+    for k, (doff, opts) in enumerate(TSO_VARIANTS):
+        for af in (4, 6):
+            for csum in ("ok", "bad"):
+                if af == 4:
+                    f = eth(ipv4(PEER4, L4A, 6, tcp(4, PEER4, L4A, 40000, 80, b"xy" * 9, doff=doff,
+                                                    options=opts, csum=csum)), 0x0800)
+                else:
+                    f = eth(ipv6(PEER6, L6A, 6, tcp(6, PEER6, L6A, 41000, 443, b"xy" * 9,
+                                                    doff=doff, options=opts, csum=csum)), 0x86DD)
+                buf, desc = pack([(f, 0)])
+                r = st.handle_rx_batch(buf, desc)[0]
+                want = k == 0 and csum == "ok"
+                assert bool(r["flags"] & _abi.F_TSO) == want, (k, af, csum, r)
