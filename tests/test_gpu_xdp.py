@@ -117,3 +117,29 @@ def test_poll_consumes_in_batches(cuda):
     assert done == n and calls == 3
     got = out.cpu().numpy().view(_abi.RESULT_DTYPE)
     assert got.tobytes() == want.tobytes(), diff_report(got, want)
+
+
+def test_ring_argument_errors(cuda):
+    """-EINVAL for a mask that is not 2^k - 1 or more entries than the ring
+    holds; n = 0 is a no-op; a poll with nothing produced consumes nothing."""
+    import errno
+    torch = cuda
+    g = GpuRxStack(device=0)
+    umem = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    ring = torch.zeros(16 * 8, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(32 * 8, dtype=torch.uint8, device="cuda")
+    for mask, n in ((6, 1), (7, 9), (0xffffffff, 1)):
+        with pytest.raises(OSError) as e:
+            g.xdp_dev(umem.data_ptr(), umem.numel(), ring.data_ptr(), mask, 0, n, 0,
+                      out.data_ptr())
+        assert e.value.errno == errno.EINVAL
+    g.xdp_dev(umem.data_ptr(), umem.numel(), ring.data_ptr(), 7, 5, 0, 0, out.data_ptr())
+    cons = np.array([123], dtype=np.uint32)
+    prod = np.array([123], dtype=np.uint32)
+    assert g.xdp_poll(umem.data_ptr(), umem.numel(), ring.data_ptr(), 7, cons, prod, 8, 0,
+                      out.data_ptr()) == 0
+    assert int(cons[0]) == 123
+    prod[0] = 125
+    assert g.xdp_poll(umem.data_ptr(), umem.numel(), ring.data_ptr(), 7, cons, prod, 0, 0,
+                      out.data_ptr()) == 0
+    assert int(cons[0]) == 123
