@@ -1252,6 +1252,8 @@ struct TxHdr {
   uint32_t ip_pos, l4_pos;  // frame offsets of the check fields
   uint32_t ip_ck;           // the IPv4 header checksum to store
   bool ip_do, l4_do, udp, longl4;
+  bool whole;       // fixed format, 64-B-aligned frame of >= 64 B: its first 64 B
+  uint4 head[4];    //   (as staged) are written back whole, check fields patched
   uint32_t s4;      // window part of the L4 region's word sum (window coordinates)
   uint32_t pseudo;  // pseudo-header words + 0xffff - old check (L4-relative)
 };
@@ -1268,6 +1270,12 @@ __device__ __forceinline__ bool tx_fixed(const uint4 (&c)[HC], int shift, int le
             (tcp || proto == 17u);
   ok = ok && (tcp ? (len >= 54 && doff4 >= 20u && (uint32_t)len >= 34u + doff4) : len >= 42);
   if (!ok) return false;
+  // A write of part of a 64-B memory granule is read-modify-written by the
+  // memory; the frame's first granule, holding both check fields, is
+  // therefore written back whole when it lies inside the frame.
+  h.whole = len >= 64 && (off0 & 63) == 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) h.head[k] = c[k];
   const uint32_t frag = bswap16(c[1].y);
   const uint32_t addrs = (c[1].z >> 16) + (c[1].w & 0xffffu) + (c[1].w >> 16) + (c[2].x & 0xffffu);
   // IPv4 header words, bytes [14, 34) without the check field [24, 26).
@@ -1316,8 +1324,10 @@ __device__ __forceinline__ TxHdr tx_general(const Win& W, int shift, int len, ui
   auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
   auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
   TxHdr h;
-  h.ip_do = h.l4_do = h.udp = h.longl4 = false;
+  h.ip_do = h.l4_do = h.udp = h.longl4 = h.whole = false;
   h.ip_pos = h.l4_pos = h.ip_ck = h.s4 = h.pseudo = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) h.head[k] = make_uint4(0, 0, 0, 0);
   if (len < 14) return h;
   const int l3 = BE16(12) == 0x8100u ? 18 : 14;  // ci_parse_rx_vlan
   const uint32_t et = BE16(l3 - 2);
@@ -1411,14 +1421,57 @@ __device__ __forceinline__ uint32_t tx_l4_check(const TxHdr& h, int shift, uint3
   return (h.udp && v == 0u) ? 0xffffu : v;
 }
 
-// The wave's four byte stores (the two check fields, little-endian as the
-// reference's u16 stores): lanes with nothing to write store to the sink, so
-// the wave always issues exactly NST_TX stores.
+__device__ __forceinline__ void lds_write16(void* p, const uint4& v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(w) : "memory");
+}
+
+// The wave's NST_TX = 8 stores.  Frames in the whole-granule form (TxHdr):
+// their first 64 B with the check fields patched in (fixed format: IPv4
+// check at 24, UDP at 40, TCP at 50), staged through the idle ring so that
+// store u writes the granules of frames 16u .. 16u + 15, four lanes per
+// granule -- whole 64-B writes.  Every other frame: the two check fields as
+// byte stores (little-endian, as the reference's u16 stores).  Lanes with
+// nothing to write store to the sink, so the count is static.  All lanes
+// active; the ring holds no DMA (the body stream has drained).
+constexpr int NST_TX = 8;
+static_assert(R >= 4, "store_checks stages 64 lanes x 64 B in the ring");
 __device__ __forceinline__ void store_checks(const KParams& P, const DescView& dv,
-                                             const TxHdr& h, uint32_t l4v, uint32_t lane) {
+                                             const TxHdr& h, uint32_t l4v, uint32_t lane,
+                                             uint4 (*ring)[64]) {
   uint8_t* const frame = reinterpret_cast<uint8_t*>(dv.abase + (uint64_t)dv.shift);
   uint8_t* const sink = P.sink + 4u * lane;
-  const bool ip = dv.valid && h.ip_do, l4 = dv.valid && h.l4_do;
+#ifdef OO_RX_ABL_TXSINK  // ablation builds only: every check to the sink
+  const bool whole = false, ip = false, l4 = false;
+  (void)frame;
+#else
+  const bool whole = dv.valid && h.whole;
+  const bool ip = dv.valid && !h.whole && h.ip_do, l4 = dv.valid && !h.whole && h.l4_do;
+#endif
+  {
+    uint4 hd[4] = {h.head[0], h.head[1], h.head[2], h.head[3]};
+    hd[1].z = (hd[1].z & 0xffff0000u) | h.ip_ck;
+    if (h.l4_do) {
+      if (h.udp) hd[2].z = (hd[2].z & 0xffff0000u) | l4v;
+      else hd[3].x = (hd[3].x & 0xffffu) | (l4v << 16);
+    }
+    // Lane p's 64 B at ring byte 64 p.
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lds_write16(&ring[lane >> 4][((lane * 4u) & 63u) + k], hd[k]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t fa = reinterpret_cast<uint64_t>(frame);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t f = 16u * u + (lane >> 2);
+      const uint4 v = lds_read16(&ring[u][lane]);
+      const bool wf = lane_get(whole ? 1u : 0u, f) != 0;
+      const uint64_t a = (uint64_t)lane_get((uint32_t)fa, f) |
+                         ((uint64_t)lane_get((uint32_t)(fa >> 32), f) << 32);
+      uint4* const dst = wf ? reinterpret_cast<uint4*>(a) + (lane & 3u)
+                            : reinterpret_cast<uint4*>(P.sink) + lane;
+      *dst = v;
+    }
+  }
   uint8_t* const pi = ip ? frame + h.ip_pos : sink;
   uint8_t* const pl = l4 ? frame + h.l4_pos : sink + 2;
   pi[0] = (uint8_t)h.ip_ck;
@@ -1517,7 +1570,7 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
 // true): the same staging and body stream, different header work and stores.
 template <bool TX>
 __device__ __forceinline__ void tile_loop(const KParams& P) {
-  constexpr int NSTK = TX ? 4 : NST;  // stores per tile
+  constexpr int NSTK = TX ? NST_TX : NST;  // stores per tile
   // All LDS in one __shared__ array (a second object can make hipcc wait
   // vmcnt(0) before LDS reads while LDS-DMA is in flight).
   __shared__ __attribute__((aligned(16))) uint4 smem[WAVES * WAVE_U4];
@@ -1634,7 +1687,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 
     const uint32_t body = lane_get(cc.bs, myslot);
     if constexpr (TX) {
-      store_checks(P, dv, th, tx_l4_check(th, dv.shift, body), lane);
+      store_checks(P, dv, th, tx_l4_check(th, dv.shift, body), lane, L.ring);
     } else {
       finish(ps, body);
       if (P.counters != nullptr && dv.valid)
