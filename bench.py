@@ -61,6 +61,9 @@ def main() -> None:
                     help="N>1: also time an RCCL scatter of every shard from rank 0's GPU")
     ap.add_argument("--tx", action="store_true",
                     help="also time the TX checksum fill (oo_gpu_tx_fill_dev) on the same frames")
+    ap.add_argument("--xdp", action="store_true",
+                    help="also time the AF_XDP ring path (oo_gpu_rx_xdp_dev): the same frames in "
+                         "a UMEM of 2048-B buffers at 256 B headroom, struct xdp_desc ring entries")
     ap.add_argument("--host-path", action="store_true",
                     help="also time pinned H2D + transform + D2H (printed to stderr)")
     args = ap.parse_args()
@@ -170,6 +173,11 @@ def main() -> None:
         tx = time_tx_fill(torch, stack, frames, d_desc, n, mean_len, sh, args.steps, args.warmup)
         log(f"[rank {rank}] tx fill: {json.dumps(tx)}")
 
+    xdp = None
+    if args.xdp:
+        xdp = time_xdp(torch, stack, buf, desc, out, dev, sh, args.steps, args.warmup)
+        log(f"[rank {rank}] xdp ring: {json.dumps(xdp)}")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(filters, socks, buf, desc, args.cpu_seconds)
@@ -204,6 +212,8 @@ def main() -> None:
             line["host_path"] = host_path
         if tx is not None:
             line["tx_fill"] = tx
+        if xdp is not None:
+            line["xdp_ring"] = xdp
         if scatter is not None:
             line["rccl_scatter"] = scatter
         print(json.dumps(line), flush=True)
@@ -270,6 +280,63 @@ def time_tx_fill(torch, stack, frames, d_desc, n, mean_len, sh, steps, warmup):
     return {"kernel_ms": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 1),
             "achieved_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
             "bytes_per_pkt": round(bpp, 1)}
+
+
+def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=256):
+    """The transform straight off an AF_XDP RX ring: the same frames laid out
+    as AF_XDP delivers them (each in its own 2048-B UMEM buffer at `headroom`,
+    a longer frame running on into the next buffers), the ring holding the
+    entries from a consumer index just below 2^32 so the ring and the u32
+    index both wrap.  Records must equal the descriptor path's (ref_out).
+    Algorithmic bytes as the main line's: frame + 16-B entry + 32-B record."""
+    from onload_amd import _abi
+    n = len(desc)
+    lens = desc["len"].astype(np.int64)
+    nch = (headroom + lens + 2047) // 2048
+    addr = (np.concatenate(([0], np.cumsum(nch)[:-1])) * 2048 + headroom).astype(np.uint64)
+    umem = np.zeros(int(nch.sum()) * 2048, dtype=np.uint8)
+    offs = desc["frame_off"].astype(np.int64)
+    for L in np.unique(lens):  # vectorised per frame length, in bounded pieces
+        idx = np.nonzero(lens == L)[0]
+        step = max(1, (1 << 24) // max(int(L), 1))
+        col = np.arange(int(L), dtype=np.int64)
+        for i in range(0, len(idx), step):
+            j = idx[i:i + step]
+            umem[addr[j].astype(np.int64)[:, None] + col] = buf[offs[j][:, None] + col]
+    log2 = max(1, (n - 1).bit_length())
+    cons = (1 << 32) - n // 2
+    ring = np.zeros(1 << log2, dtype=_abi.XDP_DESC_DTYPE)
+    at = (cons + np.arange(n, dtype=np.uint64)) & np.uint64((1 << log2) - 1)
+    ring["addr"][at] = addr
+    ring["len"][at] = lens.astype(np.uint32)
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_ring = torch.from_numpy(ring.view(np.uint8)).to(dev)
+    del umem
+    out = torch.empty_like(ref_out)
+    intf = int(desc["intf_i"][0]) if n else 0
+
+    def run():
+        stack.xdp_dev(d_umem.data_ptr(), d_umem.numel(), d_ring.data_ptr(), (1 << log2) - 1,
+                      cons, n, intf, out.data_ptr(), 0, sh)
+    for _ in range(warmup):
+        run()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        run()
+        e.record(stream)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(out, ref_out)) and bool((desc["intf_i"] == intf).all())
+    ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    bpp = float(lens.mean()) + DESC_B + RESULT_B
+    gbs = n * bpp / (ms * 1e-3) / 1e9
+    return {"kernel_ms": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 1),
+            "achieved_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "umem_bytes": int(d_umem.numel()), "headroom": headroom,
+            "records_equal_descriptor_path": same}
 
 
 def time_host_path(torch, stack, buf, desc, dev, reps: int = 5):
