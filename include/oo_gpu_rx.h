@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OO_GPU_RX_ABI_VERSION 1
+#define OO_GPU_RX_ABI_VERSION 2
 
 /* intf_i -> hwport map size (CI_CFG_MAX_INTERFACES = 30,
  * src/include/ci/internal/transport_config_opt.h:29). */
@@ -161,8 +161,8 @@ typedef struct oo_gpu_rx_sock {
 
 typedef struct oo_gpu_rx_cfg {
   int32_t  device;            /* HIP device ordinal; < 0 = host-only context
-                                 (table mirror without a GPU; batch calls
-                                 return -ENODEV)                               */
+                                 (tables without a GPU; batch calls return
+                                 -ENODEV)                                      */
   uint32_t max_socks;         /* socket ids are 0..max_socks-1 (EP buffers)  */
   uint8_t  ip4_table_log2;    /* >= 16 (netif_table.c:280 LPRP), <= 24;
                                  default 16 (ip.h:1790-1804)                  */
@@ -170,8 +170,8 @@ typedef struct oo_gpu_rx_cfg {
   uint8_t  n_intf;            /* entries used in intf_hwport                 */
   uint8_t  rsvd;
   uint8_t  intf_hwport[OO_GPU_RX_MAX_INTF]; /* ni->state->intf_i_to_hwport   */
-  uint64_t host_stage_bytes;  /* frame staging for oo_gpu_rx_batch (0=none)  */
-  uint32_t host_stage_pkts;   /* descriptor/result staging for oo_gpu_rx_batch */
+  uint64_t host_stage_bytes;  /* frame bytes per submit slot (0 = no host path) */
+  uint32_t host_stage_pkts;   /* packets per submit slot                      */
   uint32_t rsvd2;
 } oo_gpu_rx_cfg;
 
@@ -182,15 +182,21 @@ int  oo_gpu_rx_abi_version(void);
 int  oo_gpu_rx_open(oo_gpu_rx_ctx** ctx_out, const oo_gpu_rx_cfg* cfg);
 void oo_gpu_rx_close(oo_gpu_rx_ctx* ctx);
 
-/* Filter-table mirror.  Replaces ci_netif_filter_insert / _remove
+/* Filter tables.  Replaces ci_netif_filter_insert / _remove
  * (netif_table.c:436-503 -> ci_ip4_netif_filter_insert :323-406,
  * ci_ip4_netif_filter_remove :447-495; IPv6 netif_table_ip6.c:192-345) for one
  * address family (af = 4 or 6).  Slot placement, route counts and tombstones
  * are identical to the reference.  laddr/raddr point at 4 (af 4) or 16 (af 6)
  * network-order bytes; raddr NULL means the wildcard.
  * insert: 0, -ENOBUFS (table full, :375), -EINVAL.  remove: 0 (also when the
- * filter is absent, :476-481), -EINVAL.  Changes reach the device before the
- * next batch on the context's stream. */
+ * filter is absent, :476-481), -EINVAL.
+ * The result is decided at once on a host mirror; the change itself (and a
+ * socket change, oo_gpu_rx_sock_set) is queued and applied to the HBM tables
+ * by a device kernel on the stream of the next batch (or sync_tables), in
+ * call order -- oof's deferred-op model (oof_interface.c:184-217).  Batches
+ * already enqueued on any stream of the context finish before the change
+ * lands; batches enqueued after it see it, on whatever stream.  No call
+ * synchronises with the device for it. */
 int oo_gpu_rx_table_insert(oo_gpu_rx_ctx* ctx, int af,
                            const void* laddr, uint16_t lport_be16,
                            const void* raddr, uint16_t rport_be16,
@@ -213,8 +219,27 @@ int oo_gpu_rx_table_slot(oo_gpu_rx_ctx* ctx, int af, uint32_t slot,
                          uint16_t* lport_be16);
 int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* ctx, int32_t sock_id,
                        const oo_gpu_rx_sock* sock);
-/* Push pending table/socket changes to the device on `stream` now. */
+/* Apply pending table/socket changes to the device on `stream` now. */
 int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* ctx, void* stream);
+
+/* Table image: the context's whole table state (slot records with route
+ * counts, tombstones and the socket fields they name; socket records) as one
+ * flat blob, for replicating one stack's tables onto other GPUs (SURVEY.md
+ * §8(e): broadcast once, then the same ops on every rank).  Layout: a 64-B
+ * header {u32 magic "OOTB", u32 version, u32 ip4_log2, u32 ip6_log2,
+ * u32 max_socks, u32 rsvd, u64 off_slot4, off_rc4, off_slot6, off_socks,
+ * total}, then 32-B IPv4 slot records, i32 route counts, 64-B IPv6 slot
+ * records, 48-B oo_gpu_rx_sock records.  Identical bytes from a host-only
+ * context and a device context holding the same tables.
+ * export: pending changes are applied first, then the image is copied to dst
+ * (device or host memory; host memory for a host-only context) on `stream`,
+ * asynchronously.  import: replaces the tables (pending changes dropped) from
+ * src on `stream`; returns once the mirror is loaded.  Sizes must match the
+ * context's: -EINVAL otherwise. */
+uint64_t oo_gpu_rx_table_image_bytes(const oo_gpu_rx_ctx* ctx);
+int oo_gpu_rx_table_export(oo_gpu_rx_ctx* ctx, void* dst, uint64_t bytes, void* stream);
+int oo_gpu_rx_table_import(oo_gpu_rx_ctx* ctx, const void* src, uint64_t bytes,
+                           void* stream);
 
 /* Device-resident batch: frames, descriptors and results all in HBM.
  * Enqueues the transform of n frames on `stream` and returns immediately.
@@ -278,14 +303,68 @@ int oo_gpu_rx_xdp_poll(oo_gpu_rx_ctx* ctx, const void* d_umem, uint64_t umem_byt
                        uint32_t max_n, int intf_i, oo_gpu_rx_result* d_out,
                        oo_gpu_rx_counters* d_counters, void* stream);
 
-/* Host-memory batch (the NIC ring -> socket path): copies frames and
- * descriptors host->device, runs the transform, copies results (and the
- * per-reason deltas, if `delta` is not NULL) back, and waits.  Frame bytes
- * and n must fit the staging sizes given at open.  Returns n or -errno. */
+/* Host memory the device may read and write directly (hipHostRegister,
+ * mapped): packet-buffer pools / AF_XDP UMEM and rings
+ * (efhw/af_xdp.c:463-500 registers the same memory with the kernel),
+ * result arrays.  *dev_ptr (may be NULL) receives the device address of p,
+ * for oo_gpu_rx_xdp_dev / _poll (zero-copy ingest) or process_dev.
+ * Registered frames, descriptors and results skip the pinned staging copy
+ * of oo_gpu_rx_submit.  0, -EINVAL, -ENOMEM, -ENODEV.  unregister: 0 or
+ * -ENOENT (p must be a registered base); waits for the context's batches. */
+int oo_gpu_rx_host_register(oo_gpu_rx_ctx* ctx, void* p, uint64_t bytes, void** dev_ptr);
+int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* ctx, void* p);
+
+/* Asynchronous host-memory batch (the NIC ring -> socket path): enqueues the
+ * H2D copy of frames and descriptors, the transform and the D2H copy of the
+ * results (and of the per-reason deltas, if `delta` is not NULL) on one of
+ * two staging slots, each with its own stream, so the copies of one batch
+ * overlap the transform of the other.  Unregistered buffers go through the
+ * slot's pinned staging (a host memcpy at submit for frames/descriptors, at
+ * wait for results).  Frame bytes and n must fit the staging sizes given at
+ * open.  *ticket identifies the batch.  A submit on a slot still in use
+ * completes that slot's batch first (its results land; its wait then
+ * returns -ENOENT).  submit: 0 or -errno.  wait: n, -ENOENT (unknown or
+ * already completed ticket), -EIO. */
+int oo_gpu_rx_submit(oo_gpu_rx_ctx* ctx, const void* frames, uint64_t frames_bytes,
+                     const oo_gpu_pkt_desc* desc, uint32_t n, oo_gpu_rx_result* out,
+                     oo_gpu_rx_counters* delta, uint64_t* ticket);
+int oo_gpu_rx_wait(oo_gpu_rx_ctx* ctx, uint64_t ticket);
+
+/* submit + wait.  Returns n or -errno. */
 int oo_gpu_rx_batch(oo_gpu_rx_ctx* ctx, const void* frames,
                     uint64_t frames_bytes, const oo_gpu_pkt_desc* desc,
                     uint32_t n, oo_gpu_rx_result* out,
                     oo_gpu_rx_counters* delta);
+
+/* ---------------------------------------------------------------------
+ * Host-pure checksum verifiers: the reference's public C API for this path
+ * (src/include/etherfabric/checksum.h:246-308, src/lib/ciul/checksum.c:
+ * 298-351) and ci_ip_csum_correct (netif_event.c:80-94), same argument
+ * shapes and verdicts (non-zero = correct).  No GPU, no state, no
+ * allocation: thread-safe.  Headers are the wire headers (glibc
+ * struct iphdr / udphdr / tcphdr, linux struct ipv6hdr); iov describes the
+ * L4 payload after the UDP header / the TCP header of doff*4 bytes, its
+ * elements paired across boundaries as ip_csum64_partialv (:134-159).
+ * As in the reference, an IPv4 UDP check field of 0 means "no checksum" to
+ * the caller (udp_rx.c:111-117), not to these functions. */
+struct iphdr;
+struct ipv6hdr;
+struct udphdr;
+struct tcphdr;
+struct iovec;
+int oo_rx_ip_csum_ok(const struct iphdr* ip, int max_ip_len);
+int oo_rx_udp_csum_ok(const struct iphdr* ip, const struct udphdr* udp,
+                      const struct iovec* iov, int iovlen);
+int oo_rx_udp_csum_ok_ip6(const struct ipv6hdr* ip6, const struct udphdr* udp,
+                          const struct iovec* iov, int iovlen);
+int oo_rx_tcp_csum_ok(const struct iphdr* ip, const struct tcphdr* tcp,
+                      const struct iovec* iov, int iovlen);
+int oo_rx_tcp_csum_ok_ip6(const struct ipv6hdr* ip6, const struct tcphdr* tcp,
+                          const struct iovec* iov, int iovlen);
+int oo_rx_udp_csum_ok_ipx(int af, const void* ipx, const struct udphdr* udp,
+                          const void* payload, size_t payload_len);
+int oo_rx_tcp_csum_ok_ipx(int af, const void* ipx, const struct tcphdr* tcp,
+                          const void* payload, size_t payload_len);
 
 /* Reason code -> short name ("DELIVER", "UDP_CSUM", ...). */
 const char* oo_gpu_rx_reason_str(int reason);

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboo_gpu_rx.so")
 PKTGEN_PATH = os.path.join(_HERE, "liboo_pktgen.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_INTF = 32
 
 # Reason codes (oo_gpu_rx.h), in the reference's check order.
@@ -76,6 +76,38 @@ class PgFilter(ctypes.Structure):
                 ("laddr", ctypes.c_uint8 * 16), ("raddr", ctypes.c_uint8 * 16)]
 
 
+# struct iovec (<sys/uio.h>), for the host-pure verifiers.
+class IoVec(ctypes.Structure):
+    _fields_ = [("iov_base", ctypes.c_void_p), ("iov_len", ctypes.c_size_t)]
+
+
+# Table image header (oo_gpu_rx.h, oo_gpu_rx_table_export).
+IMAGE_HDR_DTYPE = np.dtype([("magic", "<u4"), ("version", "<u4"), ("ip4_log2", "<u4"),
+                            ("ip6_log2", "<u4"), ("max_socks", "<u4"), ("rsvd0", "<u4"),
+                            ("off_slot4", "<u8"), ("off_rc4", "<u8"), ("off_slot6", "<u8"),
+                            ("off_socks", "<u8"), ("total", "<u8")])
+SLOT4_DTYPE = np.dtype([("id_state", "<u4"), ("laddr", "<u4"), ("raddr", "<u4"), ("lport", "<u2"),
+                        ("rport", "<u2"), ("proto", "u1"), ("rsvd0", "u1"), ("sflags", "<u2"),
+                        ("b2d_vlan", "<i2"), ("rsvd1", "<u2"), ("hwports", "<u8")])
+SLOT6_DTYPE = np.dtype([("id", "<i4"), ("route_count", "<i4"), ("laddr", "<u4", 4),
+                        ("raddr", "<u4", 4), ("lport", "<u2"), ("rport", "<u2"), ("proto", "u1"),
+                        ("rsvd1", "u1"), ("sflags", "<u2"), ("b2d_vlan", "<i2"), ("rsvd2", "<u2"),
+                        ("rsvd3", "<u4"), ("hwports", "<u8")])
+assert IMAGE_HDR_DTYPE.itemsize == 64 and SLOT4_DTYPE.itemsize == 32 and SLOT6_DTYPE.itemsize == 64
+
+
+def parse_image(img: np.ndarray) -> dict:
+    """Split a table image (uint8 array) into its parts."""
+    h = img[:64].view(IMAGE_HDR_DTYPE)[0]
+    n4, n6 = 1 << int(h["ip4_log2"]), 1 << int(h["ip6_log2"])
+    o4, orc, o6, os_ = (int(h[k]) for k in ("off_slot4", "off_rc4", "off_slot6", "off_socks"))
+    return {"hdr": h,
+            "slot4": img[o4:o4 + 32 * n4].view(SLOT4_DTYPE),
+            "rc4": img[orc:orc + 4 * n4].view("<i4"),
+            "slot6": img[o6:o6 + 64 * n6].view(SLOT6_DTYPE),
+            "socks": img[os_:int(h["total"])]}
+
+
 # Every symbol include/oo_gpu_rx.h declares, with its ctypes signature.
 _P, _U8, _U16, _U32, _U64, _I32 = (ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16,
                                    ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32)
@@ -97,6 +129,20 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_xdp_poll": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _U32, ctypes.c_int,
                                           _P, _P, _P]),
     "oo_gpu_rx_batch": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P]),
+    "oo_gpu_rx_submit": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, ctypes.POINTER(_U64)]),
+    "oo_gpu_rx_wait": (ctypes.c_int, [_P, _U64]),
+    "oo_gpu_rx_host_register": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_P)]),
+    "oo_gpu_rx_host_unregister": (ctypes.c_int, [_P, _P]),
+    "oo_gpu_rx_table_image_bytes": (_U64, [_P]),
+    "oo_gpu_rx_table_export": (ctypes.c_int, [_P, _P, _U64, _P]),
+    "oo_gpu_rx_table_import": (ctypes.c_int, [_P, _P, _U64, _P]),
+    "oo_rx_ip_csum_ok": (ctypes.c_int, [_P, ctypes.c_int]),
+    "oo_rx_udp_csum_ok": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "oo_rx_udp_csum_ok_ip6": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "oo_rx_tcp_csum_ok": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "oo_rx_tcp_csum_ok_ip6": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "oo_rx_udp_csum_ok_ipx": (ctypes.c_int, [ctypes.c_int, _P, _P, _P, ctypes.c_size_t]),
+    "oo_rx_tcp_csum_ok_ipx": (ctypes.c_int, [ctypes.c_int, _P, _P, _P, ctypes.c_size_t]),
     "oo_gpu_rx_reason_str": (ctypes.c_char_p, [ctypes.c_int]),
 }
 

@@ -2,9 +2,11 @@
 //
 // oo_gpu_rx.cpp -- host side of the C ABI declared in include/oo_gpu_rx.h:
 // context lifetime, the filter-table mirror (insert/remove with the
-// reference's slot placement, route counts and tombstones), incremental
-// upload of the mirror to HBM, and the batch entry points that launch the
-// gfx950 kernel in oo_rx_kernel.hip.
+// reference's slot placement, route counts and tombstones), the op queue
+// that carries every table change to the device copy (applied there by
+// oo_table_kernel.hip on the batch stream), cross-stream ordering, the
+// device-resident / AF_XDP / TX entry points, and the asynchronous
+// host-memory path (pinned staging, two streams, double-buffered).
 //
 // Table semantics restated from (file:line in /root/reference):
 //   ci_ip4_netif_filter_insert        src/lib/transport/ip/netif_table.c:323-406
@@ -27,43 +29,40 @@
 
 #include "oo_rx_device.h"
 
-extern "C" int oo_rx_launch(const oo_rx::KParams* P, int split, int grid, hipStream_t stream);
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_tx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
-extern "C" int oo_rx_blocks_per_cu(int split);
-extern "C" int oo_rx_waves_per_block(int split);
+extern "C" int oo_rx_blocks_per_cu(void);
+extern "C" int oo_rx_waves_per_block(void);
+extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
+                                   uint32_t n, uint32_t gen, hipStream_t s);
+extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s);
+extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s);
+extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s);
 
 namespace {
 
-using oo_rx::Ip6Entry;
+using oo_rx::DevTables;
+using oo_rx::hash2;
+using oo_rx::hash3;
+using oo_rx::ID6_EMPTY;
+using oo_rx::ID6_TOMBSTONE;
+using oo_rx::ID_MASK;
 using oo_rx::KParams;
+using oo_rx::occupied;
 using oo_rx::Slot4;
 using oo_rx::Slot6;
-
-constexpr uint32_t ST_MASK = 0xc0000000u;
-constexpr uint32_t ID_MASK = 0x3fffffffu;
-constexpr uint32_t ST_PREFERRED = 0x00000000u;
-constexpr uint32_t ST_REHASHED = 0x40000000u;
-constexpr uint32_t ST_EMPTY = 0x80000000u;
-constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
-constexpr int32_t ID6_TOMBSTONE = -1;
-constexpr int32_t ID6_EMPTY = -2;
+using oo_rx::ST_EMPTY;
+using oo_rx::ST_MASK;
+using oo_rx::ST_PREFERRED;
+using oo_rx::ST_REHASHED;
+using oo_rx::ST_TOMBSTONE;
+using oo_rx::TableOp;
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* v = getenv(name);
   return (v && *v) ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
 }
 
-inline bool occupied(uint32_t st) { return ((~st) & ST_EMPTY & ST_TOMBSTONE) != 0; }
-
-inline uint32_t hash3(uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp, uint32_t proto) {
-  uint32_t h = __builtin_bswap32(ra) ^ la ^ ((rp << 16) | lp) ^ proto;
-  h ^= h >> 16;
-  h ^= h >> 8;
-  return h;
-}
-inline uint32_t hash2(uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp, uint32_t proto) {
-  return ((la ^ ra) ^ ((lp << 16) | rp) ^ proto) | 1u;
-}
 inline uint32_t ld32(const void* p) {
   uint32_t v;
   memcpy(&v, p, 4);
@@ -74,24 +73,8 @@ inline uint32_t addr_xor(const void* a16) {
   return ld32(a) ^ ld32(a + 4) ^ ld32(a + 8) ^ ld32(a + 12);
 }
 
-// [lo, hi) range of entries changed since the last upload.
-struct Dirty {
-  uint32_t lo = UINT32_MAX, hi = 0;
-  void mark(uint32_t i) {
-    lo = std::min(lo, i);
-    hi = std::max(hi, i + 1);
-  }
-  void all(uint32_t n) {
-    lo = 0;
-    hi = n;
-  }
-  bool any() const { return hi > lo; }
-  void clear() {
-    lo = UINT32_MAX;
-    hi = 0;
-  }
-};
-
+// ci_netif_filter_table_entry_fast {id|state, laddr} and _ext
+// {route_count, lport} (ip_shared_types.h:533-563).
 struct Entry4 {
   uint32_t id_state, laddr;
 };
@@ -99,7 +82,62 @@ struct Ext4 {
   int32_t route_count;
   uint16_t lport, pad;
 };
-static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8, "v4 entry layout");
+// ci_ip6_netif_filter_table_entry {id, route_count, laddr[16]}
+// (ip_shared_types.h:579-583).
+struct Entry6 {
+  int32_t id;
+  int32_t route_count;
+  uint32_t laddr[4];
+};
+static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
+              "entry layouts");
+
+constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
+constexpr int NTRACK = 8;             // streams whose last launch is tracked
+constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
+
+// The last launch on one stream (cross-stream ordering of table changes).
+struct Tracked {
+  hipStream_t s = nullptr;
+  hipEvent_t ev = nullptr;
+  bool live = false;      // ev recorded since the last table flush waited on it
+  uint32_t tables_seen = 0;  // table generation this stream has waited for
+  uint64_t lru = 0;
+};
+
+// One op-flush staging buffer: pinned host ops -> device ops, reused once
+// the kernel that read it has finished (ev).
+struct OpStage {
+  TableOp* h = nullptr;
+  TableOp* d = nullptr;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+
+// One host-path staging slot (oo_gpu_rx_submit / _wait).
+struct HostSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* d_frames = nullptr;
+  oo_gpu_pkt_desc* d_desc = nullptr;
+  oo_gpu_rx_result* d_out = nullptr;
+  uint32_t* d_ctr = nullptr;
+  uint8_t* h_frames = nullptr;  // pinned
+  oo_gpu_pkt_desc* h_desc = nullptr;
+  oo_gpu_rx_result* h_out = nullptr;
+  uint32_t* h_ctr = nullptr;
+  bool busy = false;
+  uint64_t ticket = 0;
+  uint32_t n = 0;
+  oo_gpu_rx_result* out = nullptr;  // caller's buffer
+  oo_gpu_rx_counters* delta = nullptr;
+  bool copy_out = false;  // out is not registered: copy from h_out at wait
+};
+
+struct HostReg {
+  uintptr_t lo, hi;
+  void* dev;
+};
 
 }  // namespace
 
@@ -107,40 +145,62 @@ struct oo_gpu_rx_ctx {
   int device = 0;
   uint32_t ip4_mask = 0, ip6_mask = 0, max_socks = 0;
   uint8_t hwport[OO_GPU_RX_MAX_INTF];
+  // host mirror (authoritative for the calls that return at once)
   std::vector<Entry4> ip4;
   std::vector<Ext4> ip4_ext;
-  std::vector<Ip6Entry> ip6;
+  std::vector<Entry6> ip6;
   std::vector<oo_gpu_rx_sock> socks;
-  Dirty dirty_ip4, dirty_ip6, dirty_socks;
-  // Device layout (oo_rx_device.h): slot records + not-EMPTY bitmaps, built
-  // from the mirror above at sync time.
-  std::vector<Slot4> slot4;
-  std::vector<uint32_t> occ4;
-  std::vector<Slot6> slot6;
-  std::vector<uint32_t> occ6;
-  Slot4* d_slot4 = nullptr;
-  uint32_t* d_occ4 = nullptr;
-  Slot6* d_slot6 = nullptr;
-  uint32_t* d_occ6 = nullptr;
-  uint8_t* d_zero = nullptr;  // oo_rx::ZERO_LINES x 16 B of zeros
+  // device copy and the ops that have not reached it yet
+  DevTables T = {};
+  std::vector<TableOp> ops;
+  bool ops_sock = false;  // ops holds an OP_SOCK (a refresh pass follows)
+  uint32_t gen = 1;       // flush generation (sockgen marks)
+  uint32_t tables_gen = 0;  // flushes done; streams wait for it via tables_ev
+  hipEvent_t tables_ev = nullptr;
+  hipStream_t tables_stream = nullptr;
+  OpStage stage[2];
+  int stage_next = 0;
+  Tracked track[NTRACK];
+  uint64_t lru = 0;
+  uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros + the sink
   uint32_t grid = 1024;        // resident blocks of rx_kernel
-  uint32_t grid_split = 1024;  // resident blocks of rx_split
-  uint32_t tstep = 8;                // tile size step (KParams::tstep)
-  uint32_t split_min = 0xffffffffu;  // mean bytes per frame from which rx_split runs (never:
-                                     // rx_kernel measured as fast or faster on configs 2-5)
-  int kernel_force = -1;       // OO_RX_KERNEL: 0 = rx_kernel, 1 = rx_split
+  uint32_t tstep = 8;          // tile size step (KParams::tstep)
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
-  // host-path staging
+  // host path
   uint64_t stage_bytes = 0;
   uint32_t stage_pkts = 0;
-  uint8_t* d_stage_frames = nullptr;
-  oo_gpu_pkt_desc* d_stage_desc = nullptr;
-  oo_gpu_rx_result* d_stage_out = nullptr;
-  uint32_t* d_stage_ctr = nullptr;
-  hipStream_t stream = nullptr;
+  HostSlot slot[NSLOT];
+  uint64_t next_ticket = 1;
+  std::vector<HostReg> regs;
+  hipStream_t stream = nullptr;  // the context's own stream (setup work)
+  uint8_t* h_image_hdr = nullptr;  // pinned 64-B table image header
 };
 
 namespace {
+
+bool has_dev(const oo_gpu_rx_ctx* c) { return c->device >= 0; }
+
+void push_op(oo_gpu_rx_ctx* c, const TableOp& op) {
+  if (!has_dev(c)) return;
+  c->ops.push_back(op);
+  if (op.kind == oo_rx::OP_SOCK) c->ops_sock = true;
+}
+
+TableOp tuple_op(uint8_t kind, int af, const void* la, uint16_t lp, const void* ra, uint16_t rp,
+                 uint8_t proto, int32_t id) {
+  TableOp op;
+  memset(&op, 0, sizeof(op));
+  op.kind = kind;
+  op.af = (uint8_t)af;
+  op.proto = proto;
+  op.lport = lp;
+  op.rport = rp;
+  op.sock = id;
+  const size_t n = af == 4 ? 4 : 16;
+  memcpy(op.u.t.la, la, n);
+  if (ra) memcpy(op.u.t.ra, ra, n);
+  return op;
+}
 
 // ---- IPv4 mirror: netif_table.c:323-495.
 int ip4_insert(oo_gpu_rx_ctx* c, int32_t id, uint32_t la, uint32_t lp, uint32_t ra,
@@ -150,14 +210,12 @@ int ip4_insert(oo_gpu_rx_ctx* c, int32_t id, uint32_t la, uint32_t lp, uint32_t 
   const uint32_t first = h1;
   while (occupied(c->ip4[h1].id_state)) {
     ++c->ip4_ext[h1].route_count;
-    c->dirty_ip4.mark(h1);
     h1 = (h1 + h2) & c->ip4_mask;
     if (h1 == first) return -ENOBUFS;  // route counts stay raised (:349-376)
   }
   c->ip4[h1].id_state = (h1 == first ? ST_PREFERRED : ST_REHASHED) | ((uint32_t)id & ID_MASK);
   c->ip4[h1].laddr = la;
   c->ip4_ext[h1].lport = (uint16_t)lp;
-  c->dirty_ip4.mark(h1);
   return 0;
 }
 
@@ -182,12 +240,10 @@ void ip4_remove(oo_gpu_rx_ctx* c, int32_t id, uint32_t la, uint32_t lp, uint32_t
   for (int k = 0; k < hops; ++k) {
     if (--c->ip4_ext[i].route_count == 0 && (c->ip4[i].id_state & ST_MASK) == ST_TOMBSTONE)
       c->ip4[i].id_state = (c->ip4[i].id_state & ID_MASK) | ST_EMPTY;
-    c->dirty_ip4.mark(i);
     i = (i + h2) & c->ip4_mask;
   }
   c->ip4[i].id_state =
       (c->ip4[i].id_state & ID_MASK) | (c->ip4_ext[i].route_count == 0 ? ST_EMPTY : ST_TOMBSTONE);
-  c->dirty_ip4.mark(i);
 }
 
 int ip4_lookup(const oo_gpu_rx_ctx* c, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
@@ -220,13 +276,11 @@ int ip6_insert(oo_gpu_rx_ctx* c, int32_t id, const uint8_t* la, uint32_t lp,
   const uint32_t first = h1;
   while (c->ip6[h1].id >= 0) {
     ++c->ip6[h1].route_count;
-    c->dirty_ip6.mark(h1);
     h1 = (h1 + h2) & c->ip6_mask;
     if (h1 == first) return -ENOBUFS;
   }
   c->ip6[h1].id = id;
   memcpy(c->ip6[h1].laddr, la, 16);
-  c->dirty_ip6.mark(h1);
   return 0;
 }
 
@@ -238,7 +292,7 @@ void ip6_remove(oo_gpu_rx_ctx* c, int32_t id, const uint8_t* la, uint32_t lp,
   uint32_t i = h1;
   int hops = 0;
   for (;;) {
-    const Ip6Entry& e = c->ip6[i];
+    const Entry6& e = c->ip6[i];
     if (e.id == id) {
       if (memcmp(la, e.laddr, 16) == 0) break;
     } else if (e.id == ID6_EMPTY) {
@@ -250,13 +304,11 @@ void ip6_remove(oo_gpu_rx_ctx* c, int32_t id, const uint8_t* la, uint32_t lp,
   }
   i = h1;
   for (int k = 0; k < hops; ++k) {
-    Ip6Entry& e = c->ip6[i];
+    Entry6& e = c->ip6[i];
     if (--e.route_count == 0 && e.id == ID6_TOMBSTONE) e.id = ID6_EMPTY;
-    c->dirty_ip6.mark(i);
     i = (i + h2) & c->ip6_mask;
   }
   c->ip6[i].id = c->ip6[i].route_count == 0 ? ID6_EMPTY : ID6_TOMBSTONE;
-  c->dirty_ip6.mark(i);
 }
 
 int ip6_lookup(const oo_gpu_rx_ctx* c, const uint8_t* la, uint32_t lp, const uint8_t* ra,
@@ -283,39 +335,49 @@ int ip6_lookup(const oo_gpu_rx_ctx* c, const uint8_t* la, uint32_t lp, const uin
 
 const uint8_t kZero16[16] = {0};
 
-template <typename T>
-int upload(T* dst, const std::vector<T>& src, uint32_t lo, uint32_t hi, hipStream_t s) {
-  if (hi <= lo) return 0;
-  return hipMemcpyAsync(dst + lo, src.data() + lo, sizeof(T) * (hi - lo), hipMemcpyHostToDevice,
-                        s) == hipSuccess
-             ? 0
-             : -EIO;
+// ---- Table image (oo_gpu_rx_table_export / _import): a 64-B header, then
+// the slot records as the device holds them (Slot4 + route counts, Slot6)
+// and the socket records.
+constexpr uint32_t IMAGE_MAGIC = 0x42544f4fu;  // "OOTB"
+constexpr uint32_t IMAGE_VERSION = 1;
+struct ImageHdr {
+  uint32_t magic, version;
+  uint32_t ip4_log2, ip6_log2, max_socks, rsvd0;
+  uint64_t off_slot4, off_rc4, off_slot6, off_socks, total;
+
+};
+static_assert(sizeof(ImageHdr) == 64, "image header");
+
+int log2u(uint32_t v) { return 31 - __builtin_clz(v); }
+
+ImageHdr image_hdr(const oo_gpu_rx_ctx* c) {
+  ImageHdr h;
+  memset(&h, 0, sizeof(h));
+  const uint64_t n4 = c->ip4_mask + 1ull, n6 = c->ip6_mask + 1ull;
+  h.magic = IMAGE_MAGIC;
+  h.version = IMAGE_VERSION;
+  h.ip4_log2 = (uint32_t)log2u(c->ip4_mask + 1u);
+  h.ip6_log2 = (uint32_t)log2u(c->ip6_mask + 1u);
+  h.max_socks = c->max_socks;
+  h.off_slot4 = sizeof(ImageHdr);
+  h.off_rc4 = h.off_slot4 + n4 * sizeof(Slot4);
+  h.off_slot6 = h.off_rc4 + n4 * sizeof(int32_t);
+  h.off_socks = h.off_slot6 + n6 * sizeof(Slot6);
+  h.total = h.off_socks + (uint64_t)c->max_socks * sizeof(oo_gpu_rx_sock);
+  return h;
 }
 
-void free_dev(oo_gpu_rx_ctx* c) {
-  if (c->d_slot4) (void)hipFree(c->d_slot4);
-  if (c->d_occ4) (void)hipFree(c->d_occ4);
-  if (c->d_slot6) (void)hipFree(c->d_slot6);
-  if (c->d_occ6) (void)hipFree(c->d_occ6);
-  if (c->d_zero) (void)hipFree(c->d_zero);
-  if (c->d_stage_frames) (void)hipFree(c->d_stage_frames);
-  if (c->d_stage_desc) (void)hipFree(c->d_stage_desc);
-  if (c->d_stage_out) (void)hipFree(c->d_stage_out);
-  if (c->d_stage_ctr) (void)hipFree(c->d_stage_ctr);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
-}
-
-// Slot record i from the mirror: the entry, its ext entry and the fields of
-// the socket its id names (what netif_table.c:192-231 reads through the id).
-void build_slot4(oo_gpu_rx_ctx* c, uint32_t i) {
-  Slot4& r = c->slot4[i];
-  const Entry4& e = c->ip4[i];
+// The device record of a slot as the mirror defines it: entry fields, and
+// the fields of the socket the id names while the slot is not EMPTY (IPv4)
+// or occupied (IPv6); zero otherwise (oo_table_kernel.hip keeps the same).
+Slot4 slot4_of(const oo_gpu_rx_ctx* c, uint32_t i) {
+  Slot4 r;
   memset(&r, 0, sizeof(r));
-  r.id_state = e.id_state;
-  r.laddr = e.laddr;
+  r.id_state = c->ip4[i].id_state;
+  r.laddr = c->ip4[i].laddr;
   r.lport = c->ip4_ext[i].lport;
-  const uint32_t id = e.id_state & ID_MASK;
-  if ((e.id_state & ST_MASK) != ST_EMPTY && id < c->max_socks) {
+  const uint32_t id = r.id_state & ID_MASK;
+  if ((r.id_state & ST_MASK) != ST_EMPTY && id < c->max_socks) {
     const oo_gpu_rx_sock& k = c->socks[id];
     r.raddr = k.raddr_be32;
     r.rport = k.rport_be16;
@@ -324,13 +386,15 @@ void build_slot4(oo_gpu_rx_ctx* c, uint32_t i) {
     r.b2d_vlan = k.bind2dev_vlan;
     r.hwports = k.bind2dev_hwports;
   }
+  return r;
 }
 
-void build_slot6(oo_gpu_rx_ctx* c, uint32_t i) {
-  Slot6& r = c->slot6[i];
-  const Ip6Entry& e = c->ip6[i];
+Slot6 slot6_of(const oo_gpu_rx_ctx* c, uint32_t i) {
+  Slot6 r;
   memset(&r, 0, sizeof(r));
+  const Entry6& e = c->ip6[i];
   r.id = e.id;
+  r.route_count = e.route_count;
   memcpy(r.laddr, e.laddr, 16);
   if (e.id >= 0 && (uint32_t)e.id < c->max_socks) {
     const oo_gpu_rx_sock& k = c->socks[e.id];
@@ -342,59 +406,178 @@ void build_slot6(oo_gpu_rx_ctx* c, uint32_t i) {
     r.b2d_vlan = k.bind2dev_vlan;
     r.hwports = k.bind2dev_hwports;
   }
+  return r;
 }
 
-int sync_tables(oo_gpu_rx_ctx* c, hipStream_t s) {
-  if (c->device < 0) return -ENODEV;
-  const bool any = c->dirty_ip4.any() || c->dirty_ip6.any() || c->dirty_socks.any();
-  if (!any) return 0;
-  // Slots whose socket changed are rebuilt too.
-  if (c->dirty_socks.any()) {
-    const uint32_t lo = c->dirty_socks.lo, hi = c->dirty_socks.hi;
-    for (uint32_t i = 0; i <= c->ip4_mask; ++i) {
-      const uint32_t st = c->ip4[i].id_state;
-      const uint32_t id = st & ID_MASK;
-      if ((st & ST_MASK) != ST_EMPTY && id >= lo && id < hi) c->dirty_ip4.mark(i);
-    }
-    for (uint32_t i = 0; i <= c->ip6_mask; ++i) {
-      const int32_t id = c->ip6[i].id;
-      if (id >= 0 && (uint32_t)id >= lo && (uint32_t)id < hi) c->dirty_ip6.mark(i);
-    }
-    c->dirty_socks.clear();
+void image_from_mirror(const oo_gpu_rx_ctx* c, uint8_t* dst) {
+  const ImageHdr h = image_hdr(c);
+  memcpy(dst, &h, sizeof(h));
+  Slot4* s4 = reinterpret_cast<Slot4*>(dst + h.off_slot4);
+  int32_t* rc4 = reinterpret_cast<int32_t*>(dst + h.off_rc4);
+  Slot6* s6 = reinterpret_cast<Slot6*>(dst + h.off_slot6);
+  for (uint32_t i = 0; i <= c->ip4_mask; ++i) {
+    s4[i] = slot4_of(c, i);
+    rc4[i] = c->ip4_ext[i].route_count;
   }
-  int rc = 0;
-  if (c->dirty_ip4.any()) {
-    const uint32_t lo = c->dirty_ip4.lo, hi = c->dirty_ip4.hi;
-    for (uint32_t i = lo; i < hi; ++i) build_slot4(c, i);
-    const uint32_t wlo = lo >> 5, whi = ((hi - 1) >> 5) + 1;
-    for (uint32_t w = wlo; w < whi; ++w) {
-      uint32_t bits = 0;
-      for (uint32_t b = 0; b < 32; ++b)
-        if ((c->ip4[w * 32 + b].id_state & ST_MASK) != ST_EMPTY) bits |= 1u << b;
-      c->occ4[w] = bits;
-    }
-    rc = upload(c->d_slot4, c->slot4, lo, hi, s);
-    if (rc == 0) rc = upload(c->d_occ4, c->occ4, wlo, whi, s);
-    c->dirty_ip4.clear();
+  for (uint32_t i = 0; i <= c->ip6_mask; ++i) s6[i] = slot6_of(c, i);
+  memcpy(dst + h.off_socks, c->socks.data(), sizeof(oo_gpu_rx_sock) * c->max_socks);
+}
+
+void mirror_from_image(oo_gpu_rx_ctx* c, const uint8_t* src) {
+  const ImageHdr h = image_hdr(c);
+  const Slot4* s4 = reinterpret_cast<const Slot4*>(src + h.off_slot4);
+  const int32_t* rc4 = reinterpret_cast<const int32_t*>(src + h.off_rc4);
+  const Slot6* s6 = reinterpret_cast<const Slot6*>(src + h.off_slot6);
+  for (uint32_t i = 0; i <= c->ip4_mask; ++i) {
+    c->ip4[i].id_state = s4[i].id_state;
+    c->ip4[i].laddr = s4[i].laddr;
+    c->ip4_ext[i].lport = s4[i].lport;
+    c->ip4_ext[i].route_count = rc4[i];
   }
-  if (rc == 0 && c->dirty_ip6.any()) {
-    const uint32_t lo = c->dirty_ip6.lo, hi = c->dirty_ip6.hi;
-    for (uint32_t i = lo; i < hi; ++i) build_slot6(c, i);
-    const uint32_t wlo = lo >> 5, whi = ((hi - 1) >> 5) + 1;
-    for (uint32_t w = wlo; w < whi; ++w) {
-      uint32_t bits = 0;
-      for (uint32_t b = 0; b < 32 && w * 32 + b <= c->ip6_mask; ++b)
-        if (c->ip6[w * 32 + b].id != ID6_EMPTY) bits |= 1u << b;
-      c->occ6[w] = bits;
-    }
-    rc = upload(c->d_slot6, c->slot6, lo, hi, s);
-    if (rc == 0) rc = upload(c->d_occ6, c->occ6, wlo, whi, s);
-    c->dirty_ip6.clear();
+  for (uint32_t i = 0; i <= c->ip6_mask; ++i) {
+    c->ip6[i].id = s6[i].id;
+    c->ip6[i].route_count = s6[i].route_count;
+    memcpy(c->ip6[i].laddr, s6[i].laddr, 16);
   }
-  // Pageable sources: make sure the copies consumed the host arrays before
-  // the host can modify them again.
-  if (rc == 0 && hipStreamSynchronize(s) != hipSuccess) rc = -EIO;
-  return rc;
+  memcpy(c->socks.data(), src + h.off_socks, sizeof(oo_gpu_rx_sock) * c->max_socks);
+}
+
+// ---- Device lifetime.
+void free_dev(oo_gpu_rx_ctx* c) {
+  DevTables& T = c->T;
+  for (void* p : {(void*)T.slot4, (void*)T.rc4, (void*)T.occ4, (void*)T.slot6, (void*)T.occ6,
+                  (void*)T.socks, (void*)T.sockgen, (void*)c->d_zero})
+    if (p) (void)hipFree(p);
+  for (OpStage& st : c->stage) {
+    if (st.h) (void)hipHostFree(st.h);
+    if (st.d) (void)hipFree(st.d);
+    if (st.ev) (void)hipEventDestroy(st.ev);
+  }
+  for (HostSlot& s : c->slot) {
+    for (void* p : {(void*)s.d_frames, (void*)s.d_desc, (void*)s.d_out, (void*)s.d_ctr})
+      if (p) (void)hipFree(p);
+    for (void* p : {(void*)s.h_frames, (void*)s.h_desc, (void*)s.h_out, (void*)s.h_ctr})
+      if (p) (void)hipHostFree(p);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  for (Tracked& t : c->track)
+    if (t.ev) (void)hipEventDestroy(t.ev);
+  for (const HostReg& r : c->regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.lo));
+  if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
+  if (c->h_image_hdr) (void)hipHostFree(c->h_image_hdr);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+// The tracked entry of stream s (least recently used one reassigned; a
+// reassigned entry whose launch may still run is waited for first).
+Tracked& track_of(oo_gpu_rx_ctx* c, hipStream_t s) {
+  Tracked* victim = &c->track[0];
+  for (Tracked& t : c->track) {
+    if (t.ev != nullptr && t.s == s) {
+      t.lru = ++c->lru;
+      return t;
+    }
+    if (t.ev == nullptr) {
+      victim = &t;
+      break;
+    }
+    if (t.lru < victim->lru) victim = &t;
+  }
+  if (victim->ev == nullptr) {
+    (void)hipEventCreateWithFlags(&victim->ev, hipEventDisableTiming);
+  } else if (victim->live) {
+    (void)hipEventSynchronize(victim->ev);
+  }
+  victim->s = s;
+  victim->live = false;
+  victim->tables_seen = 0;
+  victim->lru = ++c->lru;
+  return *victim;
+}
+
+// Pending table ops -> device, on stream s: first wait for every launch on
+// another stream that may still read the tables (no batch sees a
+// half-updated table), then copy the ops through a pinned staging buffer and
+// apply them (table_ops), then refresh the socket fields of the slots whose
+// socket changed.  No host synchronisation unless a staging buffer is still
+// in use by an earlier flush that has not run.
+int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
+  if (c->ops.empty()) return 0;
+  for (Tracked& t : c->track) {
+    if (t.ev != nullptr && t.live && t.s != s) {
+      if (hipStreamWaitEvent(s, t.ev, 0) != hipSuccess) return -EIO;
+      t.live = false;
+    }
+  }
+  const uint32_t total = (uint32_t)c->ops.size();
+  for (uint32_t at = 0; at < total; at += OPS_CHUNK) {
+    const uint32_t n = std::min(OPS_CHUNK, total - at);
+    OpStage& st = c->stage[c->stage_next];
+    c->stage_next ^= 1;
+    if (st.pending && hipEventSynchronize(st.ev) != hipSuccess) return -EIO;
+    memcpy(st.h, c->ops.data() + at, sizeof(TableOp) * n);
+    if (hipMemcpyAsync(st.d, st.h, sizeof(TableOp) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        oo_table_launch_ops(&c->T, st.d, n, c->gen, s) != 0 ||
+        hipEventRecord(st.ev, s) != hipSuccess)
+      return -EIO;
+    st.pending = true;
+  }
+  if (c->ops_sock && oo_table_launch_refresh(&c->T, c->gen, s) != 0) return -EIO;
+  c->ops.clear();
+  c->ops_sock = false;
+  ++c->gen;
+  ++c->tables_gen;
+  if (hipEventRecord(c->tables_ev, s) != hipSuccess) return -EIO;
+  c->tables_stream = s;
+  track_of(c, s).tables_seen = c->tables_gen;
+  return 0;
+}
+
+// Everything a launch on stream s must follow: pending table ops, or the
+// last flush when it ran on another stream.
+int prepare(oo_gpu_rx_ctx* c, hipStream_t s) {
+  if (!c->ops.empty()) return flush_ops(c, s);
+  if (c->tables_gen == 0) return 0;
+  Tracked& t = track_of(c, s);
+  if (t.tables_seen != c->tables_gen) {
+    if (c->tables_stream != s && hipStreamWaitEvent(s, c->tables_ev, 0) != hipSuccess)
+      return -EIO;
+    t.tables_seen = c->tables_gen;
+  }
+  return 0;
+}
+
+int note_launch(oo_gpu_rx_ctx* c, hipStream_t s) {
+  Tracked& t = track_of(c, s);
+  if (hipEventRecord(t.ev, s) != hipSuccess) return -EIO;
+  t.live = true;
+  return 0;
+}
+
+bool in_reg(const oo_gpu_rx_ctx* c, const void* p, uint64_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  for (const HostReg& r : c->regs)
+    if (a >= r.lo && a <= r.hi && bytes <= r.hi - a) return true;
+  return false;
+}
+
+int alloc_host_slots(oo_gpu_rx_ctx* c) {
+  for (HostSlot& s : c->slot) {
+    const uint64_t pk = c->stage_pkts;
+    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&s.d_frames, c->stage_bytes) != hipSuccess ||
+        hipMalloc(&s.d_desc, sizeof(oo_gpu_pkt_desc) * pk) != hipSuccess ||
+        hipMalloc(&s.d_out, sizeof(oo_gpu_rx_result) * pk) != hipSuccess ||
+        hipMalloc(&s.d_ctr, sizeof(oo_gpu_rx_counters)) != hipSuccess ||
+        hipHostMalloc(&s.h_frames, c->stage_bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.h_desc, sizeof(oo_gpu_pkt_desc) * pk, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.h_out, sizeof(oo_gpu_rx_result) * pk, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.h_ctr, sizeof(oo_gpu_rx_counters), hipHostMallocDefault) != hipSuccess)
+      return -ENOMEM;
+  }
+  return 0;
 }
 
 }  // namespace
@@ -432,14 +615,8 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   try {
     c->ip4.assign(c->ip4_mask + 1, Entry4{ST_EMPTY, 0});
     c->ip4_ext.assign(c->ip4_mask + 1, Ext4{0, 0, 0});
-    c->ip6.assign(c->ip6_mask + 1, Ip6Entry{ID6_EMPTY, 0, {0, 0, 0, 0}});
+    c->ip6.assign(c->ip6_mask + 1, Entry6{ID6_EMPTY, 0, {0, 0, 0, 0}});
     c->socks.assign(c->max_socks, oo_gpu_rx_sock{});
-    if (!host_only) {
-      c->slot4.assign(c->ip4_mask + 1, Slot4{});
-      c->occ4.assign((c->ip4_mask >> 5) + 1, 0u);
-      c->slot6.assign(c->ip6_mask + 1, Slot6{});
-      c->occ6.assign((c->ip6_mask >> 5) + 1, 0u);
-    }
   } catch (...) {
     delete c;
     return -ENOMEM;
@@ -450,47 +627,48 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) {
-    // Persistent grids: every resident block (occupancy query), optionally
+    // Persistent grid: every resident block (occupancy query), optionally
     // scaled by OO_RX_GRID_PCT for tuning.
     const uint32_t pct = env_u32("OO_RX_GRID_PCT", 100);
-    const int b0 = oo_rx_blocks_per_cu(0), b1 = oo_rx_blocks_per_cu(1);
+    const int b0 = oo_rx_blocks_per_cu();
     if (b0 > 0)
       c->grid = std::max<uint32_t>(1, (uint32_t)(b0 * prop.multiProcessorCount) * pct / 100);
-    if (b1 > 0)
-      c->grid_split = std::max<uint32_t>(1, (uint32_t)(b1 * prop.multiProcessorCount) * pct / 100);
   }
-  c->split_min = env_u32("OO_RX_SPLIT_MIN", c->split_min);
   c->tstep = env_u32("OO_RX_TSTEP", 8) == 1 ? 1 : 8;
-  if (const char* k = getenv("OO_RX_KERNEL")) {
-    if (!strcmp(k, "split")) c->kernel_force = 1;
-    if (!strcmp(k, "lanes")) c->kernel_force = 0;
-  }
-  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipMalloc(&c->d_slot4, sizeof(Slot4) * c->slot4.size()) == hipSuccess &&
-            hipMalloc(&c->d_occ4, sizeof(uint32_t) * c->occ4.size()) == hipSuccess &&
-            hipMalloc(&c->d_slot6, sizeof(Slot6) * c->slot6.size()) == hipSuccess &&
-            hipMalloc(&c->d_occ6, sizeof(uint32_t) * c->occ6.size()) == hipSuccess &&
-            hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + 64u * 32u) == hipSuccess &&
-            hipMemset(c->d_zero, 0, 16u * oo_rx::ZERO_LINES) == hipSuccess;
+  DevTables& T = c->T;
+  T.ip4_mask = c->ip4_mask;
+  T.ip6_mask = c->ip6_mask;
+  T.max_socks = c->max_socks;
+  const uint64_t n4 = c->ip4_mask + 1ull, n6 = c->ip6_mask + 1ull;
+  bool ok =
+      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+      hipEventCreateWithFlags(&c->tables_ev, hipEventDisableTiming) == hipSuccess &&
+      hipMalloc(&T.slot4, sizeof(Slot4) * n4) == hipSuccess &&
+      hipMalloc(&T.rc4, sizeof(int32_t) * n4) == hipSuccess &&
+      hipMalloc(&T.occ4, sizeof(uint32_t) * ((n4 + 31) / 32)) == hipSuccess &&
+      hipMalloc(&T.slot6, sizeof(Slot6) * n6) == hipSuccess &&
+      hipMalloc(&T.occ6, sizeof(uint32_t) * ((n6 + 31) / 32)) == hipSuccess &&
+      hipMalloc(&T.socks, sizeof(oo_gpu_rx_sock) * c->max_socks) == hipSuccess &&
+      hipMalloc(&T.sockgen, sizeof(uint32_t) * c->max_socks) == hipSuccess &&
+      hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + 64u * 32u) == hipSuccess &&
+      hipHostMalloc(&c->h_image_hdr, sizeof(ImageHdr), hipHostMallocDefault) == hipSuccess &&
+      hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
+      oo_table_launch_init(&T, c->stream) == 0;
+  for (OpStage& st : c->stage)
+    ok = ok && hipHostMalloc(&st.h, sizeof(TableOp) * OPS_CHUNK, hipHostMallocDefault) == hipSuccess &&
+         hipMalloc(&st.d, sizeof(TableOp) * OPS_CHUNK) == hipSuccess &&
+         hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) == hipSuccess;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
     c->stage_pkts = cfg->host_stage_pkts;
-    ok = hipMalloc(&c->d_stage_frames, c->stage_bytes) == hipSuccess &&
-         hipMalloc(&c->d_stage_desc, sizeof(oo_gpu_pkt_desc) * c->stage_pkts) == hipSuccess &&
-         hipMalloc(&c->d_stage_out, sizeof(oo_gpu_rx_result) * c->stage_pkts) == hipSuccess &&
-         hipMalloc(&c->d_stage_ctr, sizeof(oo_gpu_rx_counters)) == hipSuccess;
+    ok = alloc_host_slots(c) == 0;
   }
+  // Every later use of the tables follows the init on the context stream.
+  ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
   if (!ok) {
     free_dev(c);
     delete c;
     return -ENOMEM;
-  }
-  c->dirty_ip4.all(c->ip4_mask + 1);
-  c->dirty_ip6.all(c->ip6_mask + 1);
-  if (sync_tables(c, c->stream) != 0) {
-    free_dev(c);
-    delete c;
-    return -EIO;
   }
   *out = c;
   return 0;
@@ -498,12 +676,12 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
 
 void oo_gpu_rx_close(oo_gpu_rx_ctx* c) {
   if (c == nullptr) return;
-  if (c->device < 0) {
+  if (!has_dev(c)) {
     delete c;
     return;
   }
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipDeviceSynchronize();  // every stream the context launched on
   free_dev(c);
   delete c;
 }
@@ -511,11 +689,18 @@ void oo_gpu_rx_close(oo_gpu_rx_ctx* c) {
 int oo_gpu_rx_table_insert(oo_gpu_rx_ctx* c, int af, const void* laddr, uint16_t lport,
                            const void* raddr, uint16_t rport, uint8_t proto, int32_t id) {
   if (c == nullptr || laddr == nullptr || id < 0 || (uint32_t)id >= c->max_socks) return -EINVAL;
-  if (af == 4) return ip4_insert(c, id, ld32(laddr), lport, raddr ? ld32(raddr) : 0, rport, proto);
-  if (af == 6)
-    return ip6_insert(c, id, static_cast<const uint8_t*>(laddr), lport,
-                      raddr ? static_cast<const uint8_t*>(raddr) : kZero16, rport, proto);
-  return -EINVAL;
+  int rc;
+  if (af == 4)
+    rc = ip4_insert(c, id, ld32(laddr), lport, raddr ? ld32(raddr) : 0, rport, proto);
+  else if (af == 6)
+    rc = ip6_insert(c, id, static_cast<const uint8_t*>(laddr), lport,
+                    raddr ? static_cast<const uint8_t*>(raddr) : kZero16, rport, proto);
+  else
+    return -EINVAL;
+  // The device replays the insert, -ENOBUFS included (its raised route
+  // counts are part of the table state).
+  push_op(c, tuple_op(oo_rx::OP_INSERT, af, laddr, lport, raddr, rport, proto, id));
+  return rc;
 }
 
 int oo_gpu_rx_table_remove(oo_gpu_rx_ctx* c, int af, const void* laddr, uint16_t lport,
@@ -528,6 +713,7 @@ int oo_gpu_rx_table_remove(oo_gpu_rx_ctx* c, int af, const void* laddr, uint16_t
                raddr ? static_cast<const uint8_t*>(raddr) : kZero16, rport, proto);
   else
     return -EINVAL;
+  push_op(c, tuple_op(oo_rx::OP_REMOVE, af, laddr, lport, raddr, rport, proto, id));
   return 0;
 }
 
@@ -563,15 +749,106 @@ int oo_gpu_rx_table_slot(oo_gpu_rx_ctx* c, int af, uint32_t slot, uint32_t* id_s
 int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* c, int32_t id, const oo_gpu_rx_sock* s) {
   if (c == nullptr || s == nullptr || id < 0 || (uint32_t)id >= c->max_socks) return -EINVAL;
   c->socks[id] = *s;
-  c->dirty_socks.mark((uint32_t)id);
+  TableOp op;
+  memset(&op, 0, sizeof(op));
+  op.kind = oo_rx::OP_SOCK;
+  op.sock = id;
+  op.u.s = *s;
+  push_op(c, op);
   return 0;
 }
 
 int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   if (c == nullptr) return -EINVAL;
-  if (c->device < 0) return -ENODEV;
+  if (!has_dev(c)) return -ENODEV;
   if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
-  return sync_tables(c, static_cast<hipStream_t>(stream));
+  return prepare(c, static_cast<hipStream_t>(stream));
+}
+
+uint64_t oo_gpu_rx_table_image_bytes(const oo_gpu_rx_ctx* c) {
+  return c == nullptr ? 0 : image_hdr(c).total;
+}
+
+int oo_gpu_rx_table_export(oo_gpu_rx_ctx* c, void* dst, uint64_t bytes, void* stream) {
+  if (c == nullptr || dst == nullptr) return -EINVAL;
+  const ImageHdr h = image_hdr(c);
+  if (bytes < h.total) return -EINVAL;
+  if (!has_dev(c)) {
+    image_from_mirror(c, static_cast<uint8_t*>(dst));
+    return 0;
+  }
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = prepare(c, s);
+  if (rc) return rc;
+  uint8_t* d = static_cast<uint8_t*>(dst);
+  const uint64_t n4 = c->ip4_mask + 1ull, n6 = c->ip6_mask + 1ull;
+  if (hipStreamSynchronize(s) != hipSuccess) return -EIO;  // h_image_hdr reuse
+  memcpy(c->h_image_hdr, &h, sizeof(h));
+  const bool ok =
+      hipMemcpyAsync(d, c->h_image_hdr, sizeof(h), hipMemcpyDefault, s) == hipSuccess &&
+      hipMemcpyAsync(d + h.off_slot4, c->T.slot4, sizeof(Slot4) * n4, hipMemcpyDefault, s) ==
+          hipSuccess &&
+      hipMemcpyAsync(d + h.off_rc4, c->T.rc4, sizeof(int32_t) * n4, hipMemcpyDefault, s) ==
+          hipSuccess &&
+      hipMemcpyAsync(d + h.off_slot6, c->T.slot6, sizeof(Slot6) * n6, hipMemcpyDefault, s) ==
+          hipSuccess &&
+      hipMemcpyAsync(d + h.off_socks, c->T.socks, sizeof(oo_gpu_rx_sock) * c->max_socks,
+                     hipMemcpyDefault, s) == hipSuccess;
+  if (!ok) return -EIO;
+  return note_launch(c, s);  // the copies read the tables like a batch
+}
+
+int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, void* stream) {
+  if (c == nullptr || src == nullptr) return -EINVAL;
+  const ImageHdr h = image_hdr(c);
+  if (bytes < h.total) return -EINVAL;
+  ImageHdr got;
+  std::vector<uint8_t> host;
+  if (!has_dev(c)) {
+    memcpy(&got, src, sizeof(got));
+    if (memcmp(&got, &h, sizeof(h)) != 0) return -EINVAL;
+    mirror_from_image(c, static_cast<const uint8_t*>(src));
+    return 0;
+  }
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  try {
+    host.resize(h.total);
+  } catch (...) {
+    return -ENOMEM;
+  }
+  // Setup-time call: the image comes to the host once for the mirror, and
+  // the device arrays are copied on the stream after every earlier use.
+  c->ops.clear();
+  c->ops_sock = false;
+  for (Tracked& t : c->track)
+    if (t.ev != nullptr && t.live && t.s != s && hipStreamWaitEvent(s, t.ev, 0) != hipSuccess)
+      return -EIO;
+  if (hipMemcpyAsync(host.data(), src, h.total, hipMemcpyDefault, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return -EIO;
+  memcpy(&got, host.data(), sizeof(got));
+  if (memcmp(&got, &h, sizeof(h)) != 0) return -EINVAL;
+  mirror_from_image(c, host.data());
+  const uint8_t* d = static_cast<const uint8_t*>(src);
+  const uint64_t n4 = c->ip4_mask + 1ull, n6 = c->ip6_mask + 1ull;
+  const bool ok =
+      hipMemcpyAsync(c->T.slot4, d + h.off_slot4, sizeof(Slot4) * n4, hipMemcpyDefault, s) ==
+          hipSuccess &&
+      hipMemcpyAsync(c->T.rc4, d + h.off_rc4, sizeof(int32_t) * n4, hipMemcpyDefault, s) ==
+          hipSuccess &&
+      hipMemcpyAsync(c->T.slot6, d + h.off_slot6, sizeof(Slot6) * n6, hipMemcpyDefault, s) ==
+          hipSuccess &&
+      hipMemcpyAsync(c->T.socks, d + h.off_socks, sizeof(oo_gpu_rx_sock) * c->max_socks,
+                     hipMemcpyDefault, s) == hipSuccess &&
+      oo_table_launch_occ(&c->T, s) == 0;
+  if (!ok) return -EIO;
+  ++c->tables_gen;
+  if (hipEventRecord(c->tables_ev, s) != hipSuccess) return -EIO;
+  c->tables_stream = s;
+  track_of(c, s).tables_seen = c->tables_gen;
+  return 0;
 }
 
 // tx: the TX checksum fill (tx_kernel) instead of the RX transform.
@@ -598,27 +875,20 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.n = n;
   P.ip4_mask = c->ip4_mask;
   P.ip6_mask = c->ip6_mask;
-  P.slot4 = c->d_slot4;
-  P.occ4 = c->d_occ4;
-  P.slot6 = c->d_slot6;
-  P.occ6 = c->d_occ6;
+  P.slot4 = c->T.slot4;
+  P.occ4 = c->T.occ4;
+  P.slot6 = c->T.slot6;
+  P.occ6 = c->T.occ6;
   P.zero = c->d_zero;
   P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
   P.stamps = c->stamps;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
-  // rx_split (parser + streamer waves) for large frames, rx_kernel otherwise;
-  // the frame buffer's bytes per descriptor estimate the mean frame size.
-  const int split = tx ? 0
-                 : c->kernel_force >= 0 ? c->kernel_force
-                                        : (frames_bytes >= (uint64_t)c->split_min * n ? 1 : 0);
-  // Static balanced partition: the W tile-processing waves (rx_split's
-  // streamers) each take K = ceil(n / (64 W)) tiles; NT = W K tiles of tlo or
-  // tlo + 8 packets (multiples of 8, at most 64), the last taking the < 8
-  // left over.  Small batches use fewer blocks.
-  const uint32_t wpb = (uint32_t)oo_rx_waves_per_block(split);
+  // Static balanced partition: the W waves each take K = ceil(n / (64 W))
+  // tiles; NT = W K tiles of tlo or tlo + 8 packets (multiples of 8, at most
+  // 64), the last taking the < 8 left over.  Small batches use fewer blocks.
+  const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full
-  const uint32_t cap = split ? c->grid_split : c->grid;
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, cap));
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
   const uint64_t K = (n + 64 * W - 1) / (64 * W);
   const uint64_t NT = W * K;
@@ -629,8 +899,9 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.ta = (uint32_t)std::min<uint64_t>(NT, (n - tlo * NT) / step);
   P.tstep = (uint32_t)step;
   const int grid = (int)blocks;
-  if (tx) return oo_tx_launch(&P, grid, s) == 0 ? 0 : -EIO;
-  return oo_rx_launch(&P, split, grid, s) == 0 ? 0 : -EIO;
+  const int rc = tx ? oo_tx_launch(&P, grid, s) : oo_rx_launch(&P, grid, s);
+  if (rc != 0) return -EIO;
+  return note_launch(c, s);
 }
 
 int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
@@ -638,11 +909,11 @@ int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frame
                           oo_gpu_rx_counters* d_counters, void* stream) {
   if (c == nullptr || (n > 0 && (d_frames == nullptr || d_desc == nullptr || d_out == nullptr)))
     return -EINVAL;
-  if (c->device < 0) return -ENODEV;
+  if (!has_dev(c)) return -ENODEV;
   if (n == 0) return 0;
   if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  int rc = sync_tables(c, s);
+  int rc = prepare(c, s);
   if (rc) return rc;
   return launch(c, d_frames, frames_bytes, d_desc, n, d_out,
                 reinterpret_cast<uint32_t*>(d_counters), s);
@@ -658,11 +929,11 @@ int oo_gpu_rx_xdp_dev(oo_gpu_rx_ctx* c, const void* d_umem, uint64_t umem_bytes,
       (uint64_t)n > (uint64_t)ring_mask + 1u ||
       (n > 0 && (d_umem == nullptr || d_ring == nullptr || d_out == nullptr)))
     return -EINVAL;
-  if (c->device < 0) return -ENODEV;
+  if (!has_dev(c)) return -ENODEV;
   if (n == 0) return 0;
   if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  int rc = sync_tables(c, s);
+  int rc = prepare(c, s);
   if (rc) return rc;
   return launch(c, d_umem, umem_bytes, nullptr, n, d_out,
                 reinterpret_cast<uint32_t*>(d_counters), s, false, d_ring, ring_mask, cons,
@@ -691,44 +962,139 @@ int oo_gpu_rx_xdp_poll(oo_gpu_rx_ctx* c, const void* d_umem, uint64_t umem_bytes
 int oo_gpu_tx_fill_dev(oo_gpu_rx_ctx* c, void* d_frames, uint64_t frames_bytes,
                        const oo_gpu_pkt_desc* d_desc, uint32_t n, void* stream) {
   if (c == nullptr || (n > 0 && (d_frames == nullptr || d_desc == nullptr))) return -EINVAL;
-  if (c->device < 0) return -ENODEV;
+  if (!has_dev(c)) return -ENODEV;
   if (n == 0) return 0;
   if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
   return launch(c, d_frames, frames_bytes, d_desc, n, nullptr, nullptr,
                 static_cast<hipStream_t>(stream), true);
 }
 
+int oo_gpu_rx_host_register(oo_gpu_rx_ctx* c, void* p, uint64_t bytes, void** dev_ptr) {
+  if (c == nullptr || p == nullptr || bytes == 0) return -EINVAL;
+  if (!has_dev(c)) return -ENODEV;
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) return -ENOMEM;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipHostUnregister(p);
+    return -EIO;
+  }
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+  try {
+    c->regs.push_back(HostReg{lo, lo + bytes, d});
+  } catch (...) {
+    (void)hipHostUnregister(p);
+    return -ENOMEM;
+  }
+  if (dev_ptr) *dev_ptr = d;
+  return 0;
+}
+
+int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
+  if (c == nullptr || p == nullptr) return -EINVAL;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+  for (size_t i = 0; i < c->regs.size(); ++i) {
+    if (c->regs[i].lo != lo) continue;
+    (void)hipSetDevice(c->device);
+    // No batch may still read it.
+    for (HostSlot& s : c->slot)
+      if (s.busy) (void)hipEventSynchronize(s.done);
+    for (Tracked& t : c->track)
+      if (t.ev != nullptr && t.live) (void)hipEventSynchronize(t.ev);
+    (void)hipHostUnregister(p);
+    c->regs.erase(c->regs.begin() + (long)i);
+    return 0;
+  }
+  return -ENOENT;
+}
+
+static int complete_slot(oo_gpu_rx_ctx* c, HostSlot& s) {
+  if (hipEventSynchronize(s.done) != hipSuccess) {
+    s.busy = false;
+    return -EIO;
+  }
+  if (s.copy_out) memcpy(s.out, s.h_out, sizeof(oo_gpu_rx_result) * s.n);
+  if (s.delta) memcpy(s.delta, s.h_ctr, sizeof(oo_gpu_rx_counters));
+  s.busy = false;
+  (void)c;
+  return (int)s.n;
+}
+
+int oo_gpu_rx_submit(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes,
+                     const oo_gpu_pkt_desc* desc, uint32_t n, oo_gpu_rx_result* out,
+                     oo_gpu_rx_counters* delta, uint64_t* ticket) {
+  if (c == nullptr || ticket == nullptr ||
+      (n > 0 && (frames == nullptr || desc == nullptr || out == nullptr)))
+    return -EINVAL;
+  if (!has_dev(c)) return -ENODEV;
+  if (c->stage_pkts == 0 || n > c->stage_pkts || frames_bytes > c->stage_bytes) return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  const uint64_t t = c->next_ticket;
+  HostSlot& s = c->slot[t % NSLOT];
+  if (s.busy) {  // the slot's previous batch completes first (its results land)
+    const int rc = complete_slot(c, s);
+    if (rc < 0) return rc;
+  }
+  hipStream_t st = s.stream;
+  // Frames and descriptors: straight from registered memory, otherwise
+  // through the slot's pinned staging (so the copies are truly async).
+  const void* fsrc = frames;
+  const void* dsrc = desc;
+  if (n > 0 && !in_reg(c, frames, frames_bytes)) {
+    memcpy(s.h_frames, frames, frames_bytes);
+    fsrc = s.h_frames;
+  }
+  if (n > 0 && !in_reg(c, desc, sizeof(oo_gpu_pkt_desc) * n)) {
+    memcpy(s.h_desc, desc, sizeof(oo_gpu_pkt_desc) * n);
+    dsrc = s.h_desc;
+  }
+  s.copy_out = n > 0 && !in_reg(c, out, sizeof(oo_gpu_rx_result) * n);
+  bool ok = hipMemsetAsync(s.d_ctr, 0, sizeof(oo_gpu_rx_counters), st) == hipSuccess;
+  if (n > 0)
+    ok = ok &&
+         hipMemcpyAsync(s.d_frames, fsrc, frames_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(s.d_desc, dsrc, sizeof(oo_gpu_pkt_desc) * n, hipMemcpyHostToDevice, st) ==
+             hipSuccess;
+  if (!ok) return -EIO;
+  if (n > 0) {
+    int rc = prepare(c, st);
+    if (rc == 0) rc = launch(c, s.d_frames, frames_bytes, s.d_desc, n, s.d_out, s.d_ctr, st);
+    if (rc) return rc;
+    ok = hipMemcpyAsync(s.copy_out ? s.h_out : out, s.d_out, sizeof(oo_gpu_rx_result) * n,
+                        hipMemcpyDeviceToHost, st) == hipSuccess;
+  }
+  ok = ok && hipMemcpyAsync(s.h_ctr, s.d_ctr, sizeof(oo_gpu_rx_counters), hipMemcpyDeviceToHost,
+                            st) == hipSuccess &&
+       hipEventRecord(s.done, st) == hipSuccess;
+  if (!ok) return -EIO;
+  s.busy = true;
+  s.ticket = t;
+  s.n = n;
+  s.out = out;
+  s.delta = delta;
+  c->next_ticket = t + 1;
+  *ticket = t;
+  return 0;
+}
+
+int oo_gpu_rx_wait(oo_gpu_rx_ctx* c, uint64_t ticket) {
+  if (c == nullptr) return -EINVAL;
+  if (!has_dev(c)) return -ENODEV;
+  if (c->stage_pkts == 0) return -EINVAL;
+  HostSlot& s = c->slot[ticket % NSLOT];
+  if (s.ticket != ticket) return ticket < c->next_ticket ? -ENOENT : -EINVAL;
+  if (!s.busy) return -ENOENT;  // already waited for (or completed by a later submit)
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  return complete_slot(c, s);
+}
+
 int oo_gpu_rx_batch(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes,
                     const oo_gpu_pkt_desc* desc, uint32_t n, oo_gpu_rx_result* out,
                     oo_gpu_rx_counters* delta) {
-  if (c == nullptr || (n > 0 && (frames == nullptr || desc == nullptr || out == nullptr)))
-    return -EINVAL;
-  if (c->device < 0) return -ENODEV;
-  if (n > c->stage_pkts || frames_bytes > c->stage_bytes) return -EINVAL;
-  if (n == 0) {
-    if (delta) memset(delta, 0, sizeof(*delta));
-    return 0;
-  }
-  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
-  hipStream_t s = c->stream;
-  int rc = sync_tables(c, s);
+  uint64_t t = 0;
+  const int rc = oo_gpu_rx_submit(c, frames, frames_bytes, desc, n, out, delta, &t);
   if (rc) return rc;
-  bool ok = hipMemcpyAsync(c->d_stage_frames, frames, frames_bytes, hipMemcpyHostToDevice, s) ==
-                hipSuccess &&
-            hipMemcpyAsync(c->d_stage_desc, desc, sizeof(oo_gpu_pkt_desc) * n,
-                           hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemsetAsync(c->d_stage_ctr, 0, sizeof(oo_gpu_rx_counters), s) == hipSuccess;
-  if (!ok) return -EIO;
-  rc = launch(c, c->d_stage_frames, frames_bytes, c->d_stage_desc, n, c->d_stage_out,
-              c->d_stage_ctr, s);
-  if (rc) return rc;
-  ok = hipMemcpyAsync(out, c->d_stage_out, sizeof(oo_gpu_rx_result) * n, hipMemcpyDeviceToHost,
-                      s) == hipSuccess;
-  if (ok && delta)
-    ok = hipMemcpyAsync(delta, c->d_stage_ctr, sizeof(oo_gpu_rx_counters), hipMemcpyDeviceToHost,
-                        s) == hipSuccess;
-  if (!ok || hipStreamSynchronize(s) != hipSuccess) return -EIO;
-  return (int)n;
+  return oo_gpu_rx_wait(c, t);
 }
 
 // Diagnostic: device buffer for per-wave phase stamps written by builds with

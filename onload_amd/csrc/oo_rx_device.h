@@ -9,7 +9,39 @@
 
 #include "../../include/oo_gpu_rx.h"
 
+#ifdef __HIPCC__
+#define OO_HD __host__ __device__ __forceinline__
+#else
+#define OO_HD inline
+#endif
+
 namespace oo_rx {
+
+// Filter-table entry states (netif_table.c:34-42): IPv4 entries keep the
+// socket id in the low 30 bits and the state in the top two.
+constexpr uint32_t ST_MASK = 0xc0000000u;
+constexpr uint32_t ID_MASK = 0x3fffffffu;
+constexpr uint32_t ST_PREFERRED = 0x00000000u;
+constexpr uint32_t ST_REHASHED = 0x40000000u;
+constexpr uint32_t ST_EMPTY = 0x80000000u;
+constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
+// IPv6 entries: id >= 0 occupied (netif_table_ip6.c:10-11).
+constexpr int32_t ID6_TOMBSTONE = -1;
+constexpr int32_t ID6_EMPTY = -2;
+
+OO_HD bool occupied(uint32_t st) { return ((~st) & ST_EMPTY & ST_TOMBSTONE) != 0; }
+
+// __onload_hash3 / __onload_hash2 (src/include/onload/hash.h:84-93,
+// 165-173) on network-order values held in host integers (little-endian).
+OO_HD uint32_t hash3(uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp, uint32_t proto) {
+  uint32_t h = __builtin_bswap32(ra) ^ la ^ ((rp << 16) | lp) ^ proto;
+  h ^= h >> 16;
+  h ^= h >> 8;
+  return h;
+}
+OO_HD uint32_t hash2(uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp, uint32_t proto) {
+  return ((la ^ ra) ^ ((lp << 16) | rp) ^ proto) | 1u;
+}
 
 // Host mirror of the IPv6 filter table entry
 // ci_ip6_netif_filter_table_entry {id, route_count, laddr[16]}
@@ -51,7 +83,7 @@ static_assert(sizeof(Slot4) == 32, "v4 slot record layout");
 
 struct Slot6 {
   int32_t id;         // entry: >= 0 occupied, -1 tombstone, -2 empty
-  int32_t rsvd0;
+  int32_t route_count;  // entry
   uint32_t laddr[4];  // entry
   uint32_t raddr[4];  // socket: sock_ip6_raddr
   uint16_t lport;     // socket: sock_lport_be16
@@ -65,6 +97,42 @@ struct Slot6 {
   uint64_t hwports;   // socket: rx_bind2dev_hwports
 };
 static_assert(sizeof(Slot6) == 64, "v6 slot record layout");
+
+// One filter-table change, applied on the device in order by table_ops
+// (oo_table_kernel.hip) -- the device side of ci_netif_filter_insert /
+// _remove (netif_table.c:323-505, netif_table_ip6.c:192-345) and of a
+// socket-field update.  64 bytes.
+enum : uint8_t { OP_INSERT = 1, OP_REMOVE = 2, OP_SOCK = 3 };
+struct TableOp {
+  uint8_t kind;     // OP_*
+  uint8_t af;       // 4 or 6 (INSERT / REMOVE)
+  uint8_t proto;
+  uint8_t rsvd0;
+  uint16_t lport;   // network order
+  uint16_t rport;
+  int32_t sock;     // socket id
+  uint32_t rsvd1;
+  union {
+    struct {
+      uint32_t la[4];  // laddr (IPv4: la[0])
+      uint32_t ra[4];  // raddr, zero for the wildcard
+    } t;
+    oo_gpu_rx_sock s;  // OP_SOCK
+  } u;
+};
+static_assert(sizeof(TableOp) == 64, "table op layout");
+
+// Device-resident filter-table state of a context.
+struct DevTables {
+  Slot4* slot4;
+  int32_t* rc4;       // route counts of the IPv4 slots (the ext entries)
+  uint32_t* occ4;     // bit i: IPv4 slot i is not EMPTY
+  Slot6* slot6;
+  uint32_t* occ6;
+  oo_gpu_rx_sock* socks;
+  uint32_t* sockgen;  // flush generation of each socket's last change
+  uint32_t ip4_mask, ip6_mask, max_socks;
+};
 
 // The zero region read by lanes that have no chunk to load (64 KiB, so
 // those reads spread over the L2 channels).

@@ -31,14 +31,8 @@
 //     descriptors decide the body, so it can be in flight before the parse.
 // The verdict of a long packet adds the body sum to the window part.
 //
-// Two kernels (DESIGN.md "Kernels"):
-//   rx_split  -- large frames.  A block is one parser wave and WS streamer
-//                waves.  Streamers only stream bodies, through a ring that
-//                never drains between tiles; the parser parses the tiles the
-//                streamers are streaming and finalises the previous ones.
-//                One barrier per tile phase.
-//   rx_kernel -- any traffic (the small-frame path).  Every wave parses and
-//                streams its own tiles.
+// One kernel, rx_kernel: every wave parses and streams its own tiles
+// (DESIGN.md §2); tx_kernel runs the same tile loop for the TX fill.
 // Every frame-byte and descriptor read in the streaming code is an LDS-DMA
 // (global_load_lds_dwordx4) whose completion the wave counts itself with
 // s_waitcnt vmcnt(N); the LDS reads that follow are inline asm, because
@@ -67,27 +61,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef OO_RX_RING
 #define OO_RX_RING 4  // rx_kernel: body ring slots per wave (even)
 #endif
-#ifndef OO_RX_WS
-#define OO_RX_WS 2  // rx_split: streamer waves per block (plus one parser)
-#endif
-#ifndef OO_RX_SRING
-#define OO_RX_SRING 4  // rx_split: body ring slots per streamer (even)
-#endif
 
 constexpr int WAVES = OO_RX_WAVES;
 constexpr int R = OO_RX_RING;
 static_assert(R % 2 == 0, "rx_kernel consumes its ring two pieces at a time");
-constexpr int WS = OO_RX_WS;
-constexpr int SR = OO_RX_SRING;
 constexpr int HC = 8;                // staged header chunks per packet
 constexpr int HB = HC * 16;          // staged window bytes per packet
 
-// Filter-table entry states (netif_table.c:34-42).
-constexpr uint32_t ST_MASK = 0xc0000000u;
-constexpr uint32_t ID_MASK = 0x3fffffffu;
-constexpr uint32_t ST_PREFERRED = 0x00000000u;
-constexpr uint32_t ST_EMPTY = 0x80000000u;
-constexpr uint32_t ST_TOMBSTONE = 0xc0000000u;
 constexpr uint32_t PENDING = 0xffu;
 
 typedef const __attribute__((address_space(1))) void* gptr;
@@ -142,24 +122,6 @@ __device__ __forceinline__ void lds_read16x2(const void* p0, const void* p1, uin
 // vmcnt wait).  Call with every lane active.
 __device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
-}
-
-__device__ __forceinline__ bool occupied(uint32_t st) {
-  return ((~st) & ST_EMPTY & ST_TOMBSTONE) != 0;
-}
-
-
-// hash.h:84-93 / 165-173; network-order values in host integers.
-__device__ __forceinline__ uint32_t hash3(uint32_t la, uint32_t lp, uint32_t ra,
-                                          uint32_t rp, uint32_t proto) {
-  uint32_t h = __builtin_bswap32(ra) ^ la ^ ((rp << 16) | lp) ^ proto;
-  h ^= h >> 16;
-  h ^= h >> 8;
-  return h;
-}
-__device__ __forceinline__ uint32_t hash2(uint32_t la, uint32_t lp, uint32_t ra,
-                                          uint32_t rp, uint32_t proto) {
-  return ((la ^ ra) ^ ((lp << 16) | rp) ^ proto) | 1u;
 }
 
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
@@ -909,14 +871,6 @@ __device__ __forceinline__ void finish(Parsed& ps, uint32_t body) {
   }
 }
 
-__device__ __forceinline__ void store_record(const KParams& P, uint32_t idx,
-                                             const oo_gpu_rx_result& r) {
-  uint4* o = reinterpret_cast<uint4*>(P.out + idx);
-  const uint4* src = reinterpret_cast<const uint4*>(&r);
-  o[0] = src[0];
-  o[1] = src[1];
-}
-
 // ---------------------------------------------------------------------------
 // Body streaming engine.
 //
@@ -1120,7 +1074,7 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
 }
 
 // Tiles.  The batch is cut into P.ntiles tiles, K per tile-processing wave
-// (rx_kernel's waves, rx_split's streamers), which take tiles w, w + W, ...
+// (rx_kernel's waves), which take tiles w, w + W, ...
 // (all waves sweep the buffer together: reading one ~200-MB window at a time
 // is faster than 2560 separate contiguous ranges).  Tile sizes are multiples
 // of 8 -- tlo or tlo + 8 packets, the last tile taking the < 8 left over --
@@ -1171,7 +1125,9 @@ __device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, 
   const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
   int len = (int)(d.z & 0xffffu);
   v.intf_i = P.xdp ? P.xdp_intf : (int)(int16_t)(d.z >> 16);
-  const bool inb = v.valid && off + (uint64_t)len <= P.frames_bytes;
+  // In bounds, without the u64 wrap of off + len (an offset near 2^64 must
+  // not land before the buffer).
+  const bool inb = v.valid && off <= P.frames_bytes && (uint64_t)len <= P.frames_bytes - off;
   if (!inb) len = 0;  // a descriptor outside the buffer is an empty frame
   const uint64_t base = reinterpret_cast<uint64_t>(P.frames) + (inb ? off : 0);
   v.shift = (int)(base & 15u);
@@ -1188,21 +1144,6 @@ __device__ __forceinline__ uint64_t desc_at(const KParams& P, uint32_t i) {
 }
 __device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, uint32_t lane) {
   return desc_at(P, lane < t.cnt ? t.first + lane : lane % P.n);
-}
-
-// Per-reason counters: one global atomic per distinct reason in the wave
-// (usually one or two per tile).  Not LDS: see parse_tile.
-__device__ __forceinline__ void count_reasons(const KParams& P, bool valid, uint32_t reason) {
-  if (P.counters == nullptr) return;
-  uint64_t left = __ballot(valid);
-  while (left != 0) {
-    const uint32_t first = (uint32_t)__builtin_ctzll(left);
-    const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)reason, (int)first);
-    const uint64_t same = __ballot(valid && reason == r) & left;
-    if ((threadIdx.x & 63u) == first)
-      atomicAdd(&P.counters[r & (OO_RX_R_COUNT - 1)], (uint32_t)__popcll(same));
-    left &= ~same;
-  }
 }
 
 // Stages the tile's header windows for the parse.  Rows 0..HC-1 hold the
@@ -1714,243 +1655,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
 }
 __global__ __launch_bounds__(WAVES * 64) void tx_kernel(KParams P) { tile_loop<true>(P); }
 
-// ---------------------------------------------------------------------------
-// rx_split: one parser wave + WS streamer waves per block.
-//
-// Tile phase k of block b gives streamer i the tile (k * G + b) * WS + i.
-// In phase k each streamer streams the body of its phase-k tile while the
-// parser parses all WS of them and finalises the phase k-1 tiles, whose
-// body sums the streamers left in LDS before the barrier that ends phase
-// k-1.  A streamer's ring runs on across tiles and barriers: once its tile's
-// pieces are all issued it issues the next tile's (its descriptors are
-// fetched three phases ahead), so the stream never drains.  The parser
-// stages each tile's header windows by LDS-DMA and waits for them
-// (vmcnt(0)) in its own wave, away from the streamers' counted waits.
-
-struct StreamerLds {
-  uint4 ring[SR][64];    // body ring
-  uint4 desc[3][64];     // descriptors of tiles k, k+1, k+2 (by tile phase mod 3)
-  uint32_t bsum[2][64];  // body sums of a finished tile, by phase parity
-};
-struct SplitLds {
-  StreamerLds s[WS];
-  uint4 hdr[HC][64];  // the parser's header windows (stage_window)
-};
-static_assert(SR >= 2 && SR % 2 == 0, "a streamer consumes its ring two pieces at a time");
-
-__device__ __forceinline__ void block_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// The parser's header work for tile t: the window staged by LDS-DMA (lane
-// = packet, [chunk][packet] cells, as in rx_kernel), then the common parse.
-__device__ __forceinline__ Parsed parse_tile(const KParams& P, uint4 (*hdr)[64], const Unit& t,
-                                             uint32_t lane) {
-  uint4 d = make_uint4(0, 0, 0, 0);
-  if (lane < t.cnt) d = *reinterpret_cast<const uint4*>(desc_at(P, t.first + lane));
-  const DescView dv = desc_view(P, d, t, lane);
-  stage_window(dv, zero_line(P, t, lane), hdr, lane);
-  vm_wait<0>();
-  return parse_packet(P, window_of(hdr, lane), dv.shift, dv.len,
-                            dv.intf_i, dv.abase, dv.span);
-}
-
-#ifndef OO_RX_SPLIT_MINW
-#define OO_RX_SPLIT_MINW 0  // rx_split: minimum waves per SIMD (caps VGPRs; 0: none)
-#endif
-#if OO_RX_SPLIT_MINW > 0
-__global__ __launch_bounds__((WS + 1) * 64, OO_RX_SPLIT_MINW) void rx_split(KParams P) {
-#else
-__global__ __launch_bounds__((WS + 1) * 64) void rx_split(KParams P) {
-#endif
-  __shared__ __attribute__((aligned(16))) uint4 smem[(sizeof(SplitLds) + 15) / 16];
-  SplitLds& L = *reinterpret_cast<SplitLds*>(smem);
-  const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t G = gridDim.x;
-  const uint32_t K = (P.ntiles + G * WS - 1) / (G * WS);  // tile phases
-  auto tile_of = [&](uint32_t k, uint32_t i) { return unit_of(P, (k * G + blockIdx.x) * WS + i); };
-#ifdef OO_RX_STAMPS
-  // Diagnostic: stamps[((block * (WS + 1) + wave) * 64 + phase) * 8 + slot].
-  auto sstamp = [&](uint32_t k, int ph, uint64_t val) {
-    if (P.stamps != nullptr && lane == 0 && k < 64)
-      P.stamps[(((size_t)blockIdx.x * (WS + 1) + wave) * 64 + k) * 8 + ph] = val;
-  };
-#define SSTAMP(k, ph) sstamp((k), (ph), __builtin_amdgcn_s_memrealtime())
-#else
-#define SSTAMP(k, ph) \
-  do {                \
-  } while (0)
-#endif
-
-  if (wave < (uint32_t)WS) {
-    // ---------------- streamer
-    //
-    // The ring is always full: every slot is refilled as soon as it is
-    // read, with the issue cursor's next round or, when the issue side may
-    // not run further ahead (it stays at most one tile ahead of the consume
-    // side, and stops after the last tile), with a null piece that the
-    // consume side skips.  Slots are static (the loop is unrolled over the
-    // ring), so every wait is the same vmcnt(SR-2).
-    StreamerLds& S = L.s[wave];
-    const uint32_t i = wave;
-    glds<0>(desc_src(P, tile_of(0, i), lane), &S.desc[0][0]);
-    vm_wait<0>();
-
-    // issue side: tile ti, its jobs and cursor
-    uint32_t ti = 0, Ti = 0, issued_i = 0, myslot_i = 0;
-    uint64_t zero_i = 0;
-    Jobs Ji;
-    IssueCursor ci;
-    auto setup = [&](uint32_t k) {
-      const uint4 d = lds_read16(&S.desc[k % 3][lane]);
-      const DescView dv = desc_view(P, d, tile_of(k, i), lane);
-      Ji = jobs_setup(dv.abase, dv.span, lane, myslot_i);
-      Ti = (Ji.T + 1u) & ~1u;  // whole pairs: a tile starts on an even slot
-      zero_i = zero_line(P, tile_of(k, i), lane);
-      issue_slot(ci, Ji, 0, lane, zero_i);
-      issued_i = 0;
-    };
-    setup(0);
-    // consume side: tile phase kc
-    Jobs Jc = Ji;
-    ConsumeCursor cc;
-    consume_start(cc, Jc, lane);
-    uint32_t kc = 0, Tc = Ti, myslot_c = myslot_i, done_c = 0;
-    bool ahead = false;                 // the issue side is in tile kc + 1
-    uint32_t issued = 0, consumed = 0;  // ring pieces, nulls included
-    // Descriptors of tile t are fetched at the end of phase t - 3; a piece
-    // issued after them that has been consumed proves they landed.
-    uint32_t mark_prev = 0, mark_new = 0;
-    if (K > 1) glds<0>(desc_src(P, tile_of(1, i), lane), &S.desc[1][0]);
-    if (K > 2) glds<0>(desc_src(P, tile_of(2, i), lane), &S.desc[2][0]);
-
-    auto move_on = [&]() {  // the issue side enters tile ti + 1
-      if (ahead || ti + 1 >= K) return;
-      if (consumed <= mark_prev) vm_wait<0>();
-      ++ti;
-      setup(ti);
-      ahead = true;
-    };
-    // Issues the pair of slots u, u + 1; true: a null pair.
-    auto issue_pair = [&](uint32_t u) -> bool {
-      if (issued_i == Ti) move_on();
-      issued += 2;
-      if (issued_i < Ti) {
-        issue_round(ci, Ji, zero_i, &S.ring[u][0], lane);
-        issue_round(ci, Ji, zero_i, &S.ring[u + 1][0], lane);
-        issued_i += 2;
-        return false;
-      }
-      glds<OO_RX_BODY_AUX>(zero_i, &S.ring[u][0]);
-      glds<OO_RX_BODY_AUX>(zero_i, &S.ring[u + 1][0]);
-      return true;
-    };
-    auto tile_end = [&]() {  // phase kc's tile is consumed
-      SSTAMP(kc, 1);
-      lds_write4(&S.bsum[kc & 1][lane], lane_get(cc.bs, myslot_c));
-      if (!ahead) move_on();
-      if (ahead) {
-        Jc = Ji;
-        consume_start(cc, Jc, lane);
-        Tc = Ti;
-        myslot_c = myslot_i;
-        ahead = false;
-      } else {
-        Tc = 0;
-      }
-      done_c = 0;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      SSTAMP(kc, 2);
-      block_barrier();
-      SSTAMP(kc, 3);
-      ++kc;
-      if (kc + 2 < K) {
-        glds<0>(desc_src(P, tile_of(kc + 2, i), lane), &S.desc[(kc + 2) % 3][0]);
-        mark_prev = mark_new;
-        mark_new = issued;
-      }
-      SSTAMP(kc, 0);
-    };
-
-    SSTAMP(0, 0);
-    // The ring slot is a register and a bit per slot pair marks the null
-    // pairs (one copy of the round and tile-end code).
-    uint32_t nulls = 0;
-#pragma unroll 1
-    for (uint32_t u = 0; u < (uint32_t)SR; u += 2) nulls |= (uint32_t)issue_pair(u) << (u >> 1);
-    while (kc < K && done_c == Tc) tile_end();  // empty tiles
-    uint32_t u = 0;
-    while (kc < K) {
-      vm_wait<SR - 2>();  // the two oldest pieces: slots u, u + 1
-      uint4 v0, v1;
-      lds_read16x2(&S.ring[u][lane], &S.ring[u + 1][lane], v0, v1);
-      consumed += 2;
-      const uint32_t bit = 1u << (u >> 1);
-      if (!(nulls & bit)) {
-        consume_round(cc, Jc, v0, lane);
-        consume_round(cc, Jc, v1, lane);
-        done_c += 2;
-        while (kc < K && done_c == Tc) tile_end();
-      }
-      nulls = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)(issue_pair(u) ? (nulls | bit) : (nulls & ~bit)));
-      u = u + 2 == (uint32_t)SR ? 0u : u + 2;
-    }
-    vm_wait<0>();
-    block_barrier();  // the parser's last phase
-  } else {
-    // ---------------- parser
-    Parsed ps[WS];
-    for (uint32_t k = 0; k <= K; ++k) {
-      SSTAMP(k, 0);
-      if (k > 0) {
-#pragma unroll
-        for (int i = 0; i < WS; ++i) {
-          const Unit t = tile_of(k - 1, (uint32_t)i);
-          if (t.cnt != 0) {
-            finish(ps[i], L.s[i].bsum[(k - 1) & 1][lane]);
-            const uint32_t idx = t.first + lane;
-            const bool valid = lane < t.cnt;
-            count_reasons(P, valid, ps[i].r.reason);
-            if (valid) store_record(P, idx, ps[i].r);
-          }
-        }
-      }
-      SSTAMP(k, 1);
-      if (k < K) {
-#pragma unroll
-        for (int i = 0; i < WS; ++i) {
-          const Unit t = tile_of(k, (uint32_t)i);
-#ifdef OO_RX_ABL_NOPARSE
-          if (t.cnt != 0) ps[i] = Parsed{};
-#else
-          if (t.cnt != 0) ps[i] = parse_tile(P, L.hdr, t, lane);
-#endif
-        }
-      }
-      SSTAMP(k, 2);
-      block_barrier();
-      SSTAMP(k, 3);
-    }
-  }
-}
-
 }  // namespace oo_rx
 
-// Resident blocks per CU (sizes the persistent grids).
-extern "C" int oo_rx_blocks_per_cu(int split) {
+// Resident blocks per CU (sizes the persistent grid).
+extern "C" int oo_rx_blocks_per_cu(void) {
   int b = 0;
   const hipError_t e =
-      split ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_split, (oo_rx::WS + 1) * 64, 0)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_kernel, oo_rx::WAVES * 64, 0);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::rx_kernel, oo_rx::WAVES * 64, 0);
   return e == hipSuccess ? b : 0;
 }
 
-// Tile-processing waves per block: rx_kernel's waves, rx_split's streamers.
-extern "C" int oo_rx_waves_per_block(int split) { return split ? oo_rx::WS : oo_rx::WAVES; }
+// Tile-processing waves per block.
+extern "C" int oo_rx_waves_per_block(void) { return oo_rx::WAVES; }
 
 // Launch one TX checksum fill batch on `stream` (rx_kernel's grid).
 extern "C" int oo_tx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
@@ -1958,11 +1674,8 @@ extern "C" int oo_tx_launch(const oo_rx::KParams* P, int grid, hipStream_t strea
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Launch one batch on `stream`.
-extern "C" int oo_rx_launch(const oo_rx::KParams* P, int split, int grid, hipStream_t stream) {
-  if (split)
-    hipLaunchKernelGGL(oo_rx::rx_split, dim3(grid), dim3((oo_rx::WS + 1) * 64), 0, stream, *P);
-  else
-    hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
+// Launch one RX batch on `stream`.
+extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1,0 +1,327 @@
+// SPDX-License-Identifier: BSD-2-Clause
+//
+// oo_table_kernel.hip -- device-side filter-table maintenance (SURVEY.md
+// §8(f) row 4): the oof-driven filter inserts and removes
+// (src/lib/efthrm/oof_interface.c:184-262 -> ci_netif_filter_insert /
+// _remove) applied to the HBM copy of the tables on the batch stream, in
+// the order the stack lock saw them, with no host synchronisation.
+//
+//   ci_ip4_netif_filter_insert    src/lib/transport/ip/netif_table.c:323-406
+//   __ci_ip4_netif_filter_remove  netif_table.c:409-443
+//   ci_ip4_netif_filter_remove    netif_table.c:447-495
+//   ci_ip6_netif_filter_insert    src/lib/transport/ip/netif_table_ip6.c:192-262
+//   ci_ip6_netif_filter_remove    netif_table_ip6.c:264-345
+//
+// The host keeps its own mirror (oo_gpu_rx.cpp) for the calls that return
+// at once (insert's -ENOBUFS, exact lookups); both apply the same ops in the
+// same order, so the HBM tables equal the mirror slot for slot -- route
+// counts and tombstones included (tests/test_gpu_tables.py).
+//
+// The device slot records (oo_rx_device.h Slot4 / Slot6) also carry the
+// fields of the socket each slot's id names.  A socket change (OP_SOCK)
+// marks the socket with the flush generation; table_refresh then rewrites
+// every slot that names a marked socket -- an O(table) pass, but a GPU one
+// (2^16 + 2^14 slots) on the stream, not a host rescan.
+//
+// Table ops are rare next to batches (filter churn), and their order
+// matters, so table_ops is one wave walking the ops in order; its lane 0
+// does the probe walks (each step one dependent load, as on the CPU).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "oo_rx_device.h"
+
+namespace oo_rx {
+
+__device__ __forceinline__ void occ_set(uint32_t* occ, uint32_t i, bool on) {
+  const uint32_t b = 1u << (i & 31u);
+  occ[i >> 5] = on ? (occ[i >> 5] | b) : (occ[i >> 5] & ~b);
+}
+
+// The socket fields of slot records (what netif_table.c:192-231 reads through
+// an entry's id).
+__device__ __forceinline__ void slot4_sock(Slot4& r, const oo_gpu_rx_sock& k) {
+  r.raddr = k.raddr_be32;
+  r.rport = k.rport_be16;
+  r.proto = k.protocol;
+  r.sflags = k.flags;
+  r.b2d_vlan = k.bind2dev_vlan;
+  r.hwports = k.bind2dev_hwports;
+}
+__device__ __forceinline__ void slot4_nosock(Slot4& r) {
+  r.raddr = 0;
+  r.rport = 0;
+  r.proto = 0;
+  r.sflags = 0;
+  r.b2d_vlan = 0;
+  r.hwports = 0;
+}
+__device__ __forceinline__ void slot6_sock(Slot6& r, const oo_gpu_rx_sock& k) {
+  for (int i = 0; i < 4; ++i) {
+    uint32_t w;
+    __builtin_memcpy(&w, k.raddr6 + 4 * i, 4);
+    r.raddr[i] = w;
+  }
+  r.lport = k.lport_be16;
+  r.rport = k.rport_be16;
+  r.proto = k.protocol;
+  r.sflags = k.flags;
+  r.b2d_vlan = k.bind2dev_vlan;
+  r.hwports = k.bind2dev_hwports;
+}
+__device__ __forceinline__ void slot6_nosock(Slot6& r) {
+  for (int i = 0; i < 4; ++i) r.raddr[i] = 0;
+  r.lport = 0;
+  r.rport = 0;
+  r.proto = 0;
+  r.sflags = 0;
+  r.b2d_vlan = 0;
+  r.hwports = 0;
+}
+
+// ci_ip4_netif_filter_insert: route counts of the occupied slots passed are
+// raised (and stay raised when the table is full, :349-376).
+__device__ void ip4_insert(const DevTables& T, const TableOp& op) {
+  const uint32_t la = op.u.t.la[0], ra = op.u.t.ra[0];
+  uint32_t h1 = hash3(la, op.lport, ra, op.rport, op.proto) & T.ip4_mask;
+  const uint32_t h2 = hash2(la, op.lport, ra, op.rport, op.proto);
+  const uint32_t first = h1;
+  while (occupied(T.slot4[h1].id_state)) {
+    ++T.rc4[h1];
+    h1 = (h1 + h2) & T.ip4_mask;
+    if (h1 == first) return;  // -ENOBUFS (the host mirror reports it)
+  }
+  Slot4 r = T.slot4[h1];
+  r.id_state = (h1 == first ? ST_PREFERRED : ST_REHASHED) | ((uint32_t)op.sock & ID_MASK);
+  r.laddr = la;
+  r.lport = op.lport;
+  slot4_sock(r, T.socks[op.sock]);
+  T.slot4[h1] = r;
+  occ_set(T.occ4, h1, true);
+}
+
+// ci_ip4_netif_filter_remove + __ci_ip4_netif_filter_remove.
+__device__ void ip4_remove(const DevTables& T, const TableOp& op) {
+  const uint32_t la = op.u.t.la[0], ra = op.u.t.ra[0];
+  const uint32_t h1 = hash3(la, op.lport, ra, op.rport, op.proto) & T.ip4_mask;
+  const uint32_t h2 = hash2(la, op.lport, ra, op.rport, op.proto);
+  const uint32_t id = (uint32_t)op.sock & ID_MASK;
+  uint32_t i = h1;
+  int hops = 0;
+  for (;;) {
+    const uint32_t st = T.slot4[i].id_state;
+    if (occupied(st) && (st & ID_MASK) == id) {
+      if (T.slot4[i].laddr == la) break;
+    } else if ((st & ST_MASK) == ST_EMPTY) {
+      return;  // removes of an absent filter are allowed (:476-481)
+    }
+    i = (i + h2) & T.ip4_mask;
+    ++hops;
+    if (i == h1) return;
+  }
+  auto to_empty = [&](uint32_t k) {
+    Slot4 r = T.slot4[k];
+    r.id_state = (r.id_state & ID_MASK) | ST_EMPTY;
+    slot4_nosock(r);
+    T.slot4[k] = r;
+    occ_set(T.occ4, k, false);
+  };
+  i = h1;
+  for (int k = 0; k < hops; ++k) {
+    if (--T.rc4[i] == 0 && (T.slot4[i].id_state & ST_MASK) == ST_TOMBSTONE) to_empty(i);
+    i = (i + h2) & T.ip4_mask;
+  }
+  if (T.rc4[i] == 0) {
+    to_empty(i);
+  } else {
+    T.slot4[i].id_state = (T.slot4[i].id_state & ID_MASK) | ST_TOMBSTONE;
+  }
+}
+
+__device__ __forceinline__ uint32_t addr_xor4(const uint32_t a[4]) {
+  return a[0] ^ a[1] ^ a[2] ^ a[3];
+}
+
+__device__ __forceinline__ bool laddr6_eq(const Slot6& r, const uint32_t a[4]) {
+  return r.laddr[0] == a[0] && r.laddr[1] == a[1] && r.laddr[2] == a[2] && r.laddr[3] == a[3];
+}
+
+// ci_ip6_netif_filter_insert: the same walk over 24-B entries whose id is
+// >= 0 when occupied.
+__device__ void ip6_insert(const DevTables& T, const TableOp& op) {
+  const uint32_t lx = addr_xor4(op.u.t.la), rx = addr_xor4(op.u.t.ra);
+  uint32_t h1 = hash3(lx, op.lport, rx, op.rport, op.proto) & T.ip6_mask;
+  const uint32_t h2 = hash2(lx, op.lport, rx, op.rport, op.proto);
+  const uint32_t first = h1;
+  while (T.slot6[h1].id >= 0) {
+    ++T.slot6[h1].route_count;
+    h1 = (h1 + h2) & T.ip6_mask;
+    if (h1 == first) return;  // -ENOBUFS
+  }
+  Slot6 r = T.slot6[h1];
+  r.id = op.sock;
+  for (int k = 0; k < 4; ++k) r.laddr[k] = op.u.t.la[k];
+  slot6_sock(r, T.socks[op.sock]);
+  T.slot6[h1] = r;
+  occ_set(T.occ6, h1, true);
+}
+
+// ci_ip6_netif_filter_remove: a tombstone loses its id (-1).
+__device__ void ip6_remove(const DevTables& T, const TableOp& op) {
+  const uint32_t lx = addr_xor4(op.u.t.la), rx = addr_xor4(op.u.t.ra);
+  const uint32_t h1 = hash3(lx, op.lport, rx, op.rport, op.proto) & T.ip6_mask;
+  const uint32_t h2 = hash2(lx, op.lport, rx, op.rport, op.proto);
+  uint32_t i = h1;
+  int hops = 0;
+  for (;;) {
+    const int32_t id = T.slot6[i].id;
+    if (id == op.sock) {
+      if (laddr6_eq(T.slot6[i], op.u.t.la)) break;
+    } else if (id == ID6_EMPTY) {
+      return;
+    }
+    i = (i + h2) & T.ip6_mask;
+    ++hops;
+    if (i == h1) return;
+  }
+  auto set_id = [&](uint32_t k, int32_t nid) {
+    Slot6 r = T.slot6[k];
+    r.id = nid;
+    slot6_nosock(r);
+    T.slot6[k] = r;
+    occ_set(T.occ6, k, nid != ID6_EMPTY);
+  };
+  i = h1;
+  for (int k = 0; k < hops; ++k) {
+    if (--T.slot6[i].route_count == 0 && T.slot6[i].id == ID6_TOMBSTONE) set_id(i, ID6_EMPTY);
+    i = (i + h2) & T.ip6_mask;
+  }
+  set_id(i, T.slot6[i].route_count == 0 ? ID6_EMPTY : ID6_TOMBSTONE);
+}
+
+// The ops of one flush, in order.  One wave; lane 0 works.
+__global__ __launch_bounds__(64) void table_ops(DevTables T, const TableOp* ops, uint32_t n,
+                                                uint32_t gen) {
+  if (threadIdx.x != 0) return;
+  for (uint32_t k = 0; k < n; ++k) {
+    const TableOp op = ops[k];
+    if (op.sock < 0 || (uint32_t)op.sock >= T.max_socks) continue;  // the host rejected it
+    if (op.kind == OP_SOCK) {
+      T.socks[op.sock] = op.u.s;
+      T.sockgen[op.sock] = gen;
+    } else if (op.kind == OP_INSERT) {
+      if (op.af == 4) ip4_insert(T, op);
+      else ip6_insert(T, op);
+    } else if (op.kind == OP_REMOVE) {
+      if (op.af == 4) ip4_remove(T, op);
+      else ip6_remove(T, op);
+    }
+  }
+}
+
+// Slots whose socket changed in flush `gen` take its new fields (IPv4: every
+// slot that is not EMPTY keeps its id; IPv6: occupied slots).
+__global__ __launch_bounds__(256) void table_refresh(DevTables T, uint32_t gen) {
+  const uint32_t n4 = T.ip4_mask + 1u, n6 = T.ip6_mask + 1u;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4 + n6;
+       i += gridDim.x * blockDim.x) {
+    if (i < n4) {
+      const uint32_t st = T.slot4[i].id_state;
+      const uint32_t id = st & ID_MASK;
+      if ((st & ST_MASK) != ST_EMPTY && id < T.max_socks && T.sockgen[id] == gen) {
+        Slot4 r = T.slot4[i];
+        slot4_sock(r, T.socks[id]);
+        T.slot4[i] = r;
+      }
+    } else {
+      const uint32_t j = i - n4;
+      const int32_t id = T.slot6[j].id;
+      if (id >= 0 && (uint32_t)id < T.max_socks && T.sockgen[id] == gen) {
+        Slot6 r = T.slot6[j];
+        slot6_sock(r, T.socks[id]);
+        T.slot6[j] = r;
+      }
+    }
+  }
+}
+
+// Fresh tables: every slot EMPTY (netif_table.c:592-611: IPv4 state EMPTY,
+// netif_table_ip6.c:349-365: id -2), no sockets, no occupancy.
+__global__ __launch_bounds__(256) void table_init(DevTables T) {
+  const uint32_t n4 = T.ip4_mask + 1u, n6 = T.ip6_mask + 1u;
+  const uint32_t total = n4 + n6 + T.max_socks;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    if (i < n4) {
+      Slot4 r = {};
+      r.id_state = ST_EMPTY;
+      T.slot4[i] = r;
+      T.rc4[i] = 0;
+      if ((i & 31u) == 0) T.occ4[i >> 5] = 0;
+    } else if (i < n4 + n6) {
+      const uint32_t j = i - n4;
+      Slot6 r = {};
+      r.id = ID6_EMPTY;
+      T.slot6[j] = r;
+      if ((j & 31u) == 0) T.occ6[j >> 5] = 0;
+    } else {
+      const uint32_t k = i - n4 - n6;
+      T.socks[k] = oo_gpu_rx_sock{};
+      T.sockgen[k] = 0;
+    }
+  }
+}
+
+// Occupancy bits from the slot records (after an image import).
+__global__ __launch_bounds__(256) void table_occ(DevTables T) {
+  const uint32_t w4 = (T.ip4_mask + 1u + 31u) >> 5, w6 = (T.ip6_mask + 1u + 31u) >> 5;
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < w4 + w6;
+       w += gridDim.x * blockDim.x) {
+    uint32_t bits = 0;
+    if (w < w4) {
+      for (uint32_t b = 0; b < 32u && w * 32u + b <= T.ip4_mask; ++b)
+        if ((T.slot4[w * 32u + b].id_state & ST_MASK) != ST_EMPTY) bits |= 1u << b;
+      T.occ4[w] = bits;
+    } else {
+      const uint32_t v = w - w4;
+      for (uint32_t b = 0; b < 32u && v * 32u + b <= T.ip6_mask; ++b)
+        if (T.slot6[v * 32u + b].id != ID6_EMPTY) bits |= 1u << b;
+      T.occ6[v] = bits;
+    }
+  }
+}
+
+}  // namespace oo_rx
+
+namespace {
+int grid_for(uint32_t items) {
+  const uint32_t g = (items + 255u) / 256u;
+  return (int)(g < 1024u ? (g ? g : 1u) : 1024u);
+}
+}  // namespace
+
+extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
+                                   uint32_t n, uint32_t gen, hipStream_t s) {
+  hipLaunchKernelGGL(oo_rx::table_ops, dim3(1), dim3(64), 0, s, *T, d_ops, n, gen);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s) {
+  hipLaunchKernelGGL(oo_rx::table_refresh, dim3(grid_for(T->ip4_mask + T->ip6_mask + 2u)),
+                     dim3(256), 0, s, *T, gen);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s) {
+  hipLaunchKernelGGL(oo_rx::table_init,
+                     dim3(grid_for(T->ip4_mask + T->ip6_mask + 2u + T->max_socks)), dim3(256), 0,
+                     s, *T);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s) {
+  hipLaunchKernelGGL(oo_rx::table_occ, dim3(grid_for((T->ip4_mask + T->ip6_mask + 2u) / 32u + 2u)),
+                     dim3(256), 0, s, *T);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -120,6 +120,16 @@ class GpuRxStack:
         return self._lib.oo_gpu_rx_table_remove(self._ctx, af, la, htons(lport), ra,
                                                  htons(rport), protocol, sock_id)
 
+    def filter_remove_raw(self, sock_id, af, laddr: bytes, lport_be: int,
+                          raddr: Optional[bytes], rport_be: int, protocol: int) -> int:
+        return self._lib.oo_gpu_rx_table_remove(self._ctx, af, laddr, lport_be, raddr, rport_be,
+                                                 protocol, sock_id)
+
+    def filter_lookup_raw(self, af, laddr: bytes, lport_be: int, raddr: Optional[bytes],
+                          rport_be: int, protocol: int) -> int:
+        return self._lib.oo_gpu_rx_table_lookup(self._ctx, af, laddr, lport_be, raddr, rport_be,
+                                                 protocol)
+
     def filter_lookup(self, af: int, laddr: Addr, lport: int, raddr: Addr, rport: int,
                       protocol: int) -> int:
         la, ra = self._tuple(af, laddr, raddr)
@@ -208,6 +218,68 @@ class GpuRxStack:
                                           ctypes.c_void_p(stream or None))
         if rc < 0:
             raise OSError(-rc, "oo_gpu_rx_xdp_poll")
+        return rc
+
+    # -- table image (replication across ranks) ----------
+    def image_bytes(self) -> int:
+        return int(self._lib.oo_gpu_rx_table_image_bytes(self._ctx))
+
+    def table_export(self, dst_ptr: int, nbytes: int, stream: int = 0) -> None:
+        """Copy the table image to dst (device memory; host memory for a
+        host-only stack), asynchronously on `stream`."""
+        rc = self._lib.oo_gpu_rx_table_export(self._ctx, ctypes.c_void_p(dst_ptr), nbytes,
+                                              ctypes.c_void_p(stream or None))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_table_export")
+
+    def table_import(self, src_ptr: int, nbytes: int, stream: int = 0) -> None:
+        rc = self._lib.oo_gpu_rx_table_import(self._ctx, ctypes.c_void_p(src_ptr), nbytes,
+                                              ctypes.c_void_p(stream or None))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_table_import")
+
+    def image_host(self) -> np.ndarray:
+        """The table image in host memory (host-only stacks)."""
+        img = np.zeros(self.image_bytes(), dtype=np.uint8)
+        self.table_export(img.ctypes.data, img.nbytes)
+        return img
+
+    # -- host memory the device reads directly --------------------------
+    def host_register(self, arr: np.ndarray) -> int:
+        """hipHostRegister (mapped) the array's memory; returns its device
+        address."""
+        d = ctypes.c_void_p()
+        rc = self._lib.oo_gpu_rx_host_register(self._ctx, ctypes.c_void_p(arr.ctypes.data),
+                                               arr.nbytes, ctypes.byref(d))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_host_register")
+        return int(d.value or 0)
+
+    def host_unregister(self, arr: np.ndarray) -> None:
+        rc = self._lib.oo_gpu_rx_host_unregister(self._ctx, ctypes.c_void_p(arr.ctypes.data))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_host_unregister")
+
+    # -- asynchronous host-memory batches -------------------------------
+    def submit(self, frames: np.ndarray, desc: np.ndarray, out: np.ndarray,
+               delta: Optional[np.ndarray] = None) -> int:
+        """Enqueue one host-memory batch; returns its ticket.  frames, desc,
+        out (and delta) must stay alive and unchanged until wait()."""
+        assert out.dtype == _abi.RESULT_DTYPE and len(out) >= len(desc)
+        assert desc.dtype == _abi.DESC_DTYPE and desc.flags.c_contiguous
+        t = ctypes.c_uint64()
+        rc = self._lib.oo_gpu_rx_submit(
+            self._ctx, ctypes.c_void_p(frames.ctypes.data), frames.nbytes,
+            ctypes.c_void_p(desc.ctypes.data), len(desc), ctypes.c_void_p(out.ctypes.data),
+            ctypes.c_void_p(None if delta is None else delta.ctypes.data), ctypes.byref(t))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_submit")
+        return t.value
+
+    def wait(self, ticket: int) -> int:
+        rc = self._lib.oo_gpu_rx_wait(self._ctx, ticket)
+        if rc < 0:
+            raise OSError(-rc, "oo_gpu_rx_wait")
         return rc
 
     def handle_rx_batch(self, frames: np.ndarray, desc: np.ndarray):

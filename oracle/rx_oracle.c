@@ -836,6 +836,7 @@ void oo_or_rx_one(const oo_or_tables* t, const uint8_t* frame, int len,
 typedef struct {
   const oo_or_tables* t;
   const uint8_t* frames;
+  uint64_t frames_bytes;
   const oo_gpu_pkt_desc* d;
   oo_gpu_rx_result* out;
   uint32_t lo, hi;
@@ -845,14 +846,20 @@ static void* run_shard(void* arg)
 {
   shard_t* s = arg;
   uint32_t i;
-  for( i = s->lo; i < s->hi; ++i )
-    oo_or_rx_one(s->t, s->frames + s->d[i].frame_off, s->d[i].len,
-                 s->d[i].intf_i, &s->out[i]);
+  for( i = s->lo; i < s->hi; ++i ) {
+    /* A descriptor outside the frame buffer is an empty frame (the batch
+     * boundary's rule; the overflow-safe form of off + len <= bytes). */
+    const uint64_t off = s->d[i].frame_off;
+    if( off <= s->frames_bytes && (uint64_t)s->d[i].len <= s->frames_bytes - off )
+      oo_or_rx_one(s->t, s->frames + off, s->d[i].len, s->d[i].intf_i, &s->out[i]);
+    else
+      oo_or_rx_one(s->t, s->frames, 0, s->d[i].intf_i, &s->out[i]);
+  }
   return NULL;
 }
 
 void oo_or_rx_batch(const oo_or_tables* t, const uint8_t* frames,
-                    const oo_gpu_pkt_desc* d, uint32_t n,
+                    uint64_t frames_bytes, const oo_gpu_pkt_desc* d, uint32_t n,
                     oo_gpu_rx_result* out, int nthreads)
 {
   pthread_t th[256];
@@ -863,7 +870,8 @@ void oo_or_rx_batch(const oo_or_tables* t, const uint8_t* frames,
   if( nthreads > 256 )
     nthreads = 256;
   for( k = 0; k < nthreads; ++k ) {
-    sh[k].t = t; sh[k].frames = frames; sh[k].d = d; sh[k].out = out;
+    sh[k].t = t; sh[k].frames = frames; sh[k].frames_bytes = frames_bytes;
+    sh[k].d = d; sh[k].out = out;
     sh[k].lo = (uint32_t)((uint64_t)n * k / nthreads);
     sh[k].hi = (uint32_t)((uint64_t)n * (k + 1) / nthreads);
   }
@@ -987,7 +995,7 @@ void oo_or_xdp_batch(const oo_or_tables* t, const uint8_t* umem,
     const uint64_t rq_id = e->addr / 2048u, ofs = e->addr & 2047u;
     const int len = (int)(e->len & 0xffffu);
     const uint64_t at = rq_id * 2048u + ofs;
-    if( at + (uint64_t)len <= umem_bytes )
+    if( at <= umem_bytes && (uint64_t)len <= umem_bytes - at )
       oo_or_rx_one(t, umem + at, len, intf_i, &out[i]);
     else
       oo_or_rx_one(t, umem, 0, intf_i, &out[i]);
@@ -1000,7 +1008,7 @@ void oo_or_tx_fill_batch(uint8_t* frames, uint64_t frames_bytes,
   uint32_t i;
   for( i = 0; i < n; ++i ) {
     uint64_t off = d[i].frame_off;
-    if( off + d[i].len <= frames_bytes )
+    if( off <= frames_bytes && (uint64_t)d[i].len <= frames_bytes - off )
       oo_or_tx_fill_one(frames + off, d[i].len);
   }
 }

@@ -39,9 +39,10 @@ int  oo_or_sock_set(oo_or_tables* t, int32_t id, const oo_gpu_rx_sock* s);
 /* One frame: the whole handle_rx_csum_bad -> handle_rx_pkt -> L4 demux. */
 void oo_or_rx_one(const oo_or_tables* t, const uint8_t* frame, int len,
                   int intf_i, oo_gpu_rx_result* out);
-/* A batch over `nthreads` host threads (contiguous shards). */
+/* A batch over `nthreads` host threads (contiguous shards); a descriptor
+ * outside [0, frames_bytes) is an empty frame. */
 void oo_or_rx_batch(const oo_or_tables* t, const uint8_t* frames,
-                    const oo_gpu_pkt_desc* desc, uint32_t n,
+                    uint64_t frames_bytes, const oo_gpu_pkt_desc* desc, uint32_t n,
                     oo_gpu_rx_result* out, int nthreads);
 
 /* The batch straight off an AF_XDP RX ring (efxdp_vi.c:316-356). */

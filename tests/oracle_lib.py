@@ -41,7 +41,7 @@ def oracle():
                                           ctypes.POINTER(_I32), ctypes.POINTER(_U16)]),
             "oo_or_sock_set": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_abi.Sock)]),
             "oo_or_rx_one": (None, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
-            "oo_or_rx_batch": (None, [_P, _P, _P, _U32, _P, ctypes.c_int]),
+            "oo_or_rx_batch": (None, [_P, _P, ctypes.c_uint64, _P, _U32, _P, ctypes.c_int]),
             "oo_or_ip4_hdr_ok": (ctypes.c_int, [_P, ctypes.c_int]),
             "oo_or_udp4_ok": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t]),
             "oo_or_udp6_ok": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t]),
@@ -123,6 +123,13 @@ class OracleStack:
         return self._lib.oo_or_insert(self._t, af, laddr, lport_be, raddr, rport_be, protocol,
                                       sock_id)
 
+    def filter_remove_raw(self, sock_id, af, laddr, lport_be, raddr, rport_be, protocol):
+        return self._lib.oo_or_remove(self._t, af, laddr, lport_be, raddr, rport_be, protocol,
+                                      sock_id)
+
+    def filter_lookup_raw(self, af, laddr, lport_be, raddr, rport_be, protocol):
+        return self._lib.oo_or_lookup(self._t, af, laddr, lport_be, raddr, rport_be, protocol)
+
     def filter_remove(self, sock_id, af, laddr, lport, raddr, rport, protocol):
         return self._lib.oo_or_remove(self._t, af, addr_bytes(af, laddr), htons(lport),
                                       addr_bytes(af, raddr), htons(rport), protocol, sock_id)
@@ -151,11 +158,13 @@ class OracleStack:
                                         f.lport_be, ra, f.rport_be, f.proto)
             assert rc == 0, rc
 
-    def handle_rx_batch(self, frames: np.ndarray, desc: np.ndarray, nthreads: int = 1):
+    def handle_rx_batch(self, frames: np.ndarray, desc: np.ndarray, nthreads: int = 1,
+                        frames_bytes: int | None = None):
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         desc = np.ascontiguousarray(desc, dtype=_abi.DESC_DTYPE)
         out = np.zeros(len(desc), dtype=_abi.RESULT_DTYPE)
-        self._lib.oo_or_rx_batch(self._t, frames.ctypes.data, desc.ctypes.data, len(desc),
+        nb = frames.nbytes if frames_bytes is None else min(frames_bytes, frames.nbytes)
+        self._lib.oo_or_rx_batch(self._t, frames.ctypes.data, nb, desc.ctypes.data, len(desc),
                                  out.ctypes.data, nthreads)
         return out
 

@@ -22,11 +22,11 @@ HDR = os.path.join(ROOT, "include", "oo_gpu_rx.h")
 
 def test_header_symbols_exported():
     text = open(HDR).read()
-    declared = set(re.findall(r"\b(oo_gpu_(?:rx|tx)_\w+)\s*\(", text))
+    declared = set(re.findall(r"\b(oo_(?:gpu_(?:rx|tx)|rx)_\w+)\s*\(", text))
     assert declared == set(_abi.ABI_SYMBOLS), declared ^ set(_abi.ABI_SYMBOLS)
     out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
-    exported = set(re.findall(r" T (oo_gpu_(?:rx|tx)_\w+)", out))
+    exported = set(re.findall(r" T (oo_\w+)", out))
     assert declared <= exported, declared - exported
     lib = _abi.load_library()
     assert lib.oo_gpu_rx_abi_version() == _abi.ABI_VERSION

@@ -78,3 +78,27 @@ def test_tx_full_size_config2_then_rx(stack):
     for r in (_abi.R_IP4_CSUM, _abi.R_UDP_CSUM, _abi.R_TCP_CSUM):
         assert ctr[r] == 0
     torch.cuda.synchronize()
+
+
+def test_tx_wrapping_descriptors_write_nothing_outside(stack):
+    """Descriptors with offsets near 2^64 (offset + length wraps) and ones
+    running past the buffer are left alone: no byte outside the frame buffer
+    and no other frame changes."""
+    import torch
+    buf, desc = pack(edge_frames()[:64], align=64)
+    n = len(buf)
+    desc[2]["frame_off"] = (1 << 64) - 64
+    desc[2]["len"] = 64
+    desc[3]["frame_off"] = (1 << 64) - 16
+    desc[4]["frame_off"] = n - 8
+    guard = 1 << 16
+    big = np.full(n + 2 * guard, 0x5A, dtype=np.uint8)
+    big[guard:guard + n] = buf
+    d = torch.from_numpy(big).to("cuda")
+    de = torch.from_numpy(np.ascontiguousarray(desc).view(np.uint8)).to("cuda")
+    stack.tx_fill_dev(d.data_ptr() + guard, n, de.data_ptr(), len(desc),
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    assert (got[:guard] == 0x5A).all() and (got[guard + n:] == 0x5A).all()
+    _same(got[guard:guard + n], oracle_tx_fill(buf, desc))

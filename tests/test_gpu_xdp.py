@@ -71,6 +71,9 @@ def test_length_bits_and_outside_entries(cuda):
     ents["addr"][5] = umem.nbytes - 7
     ents["addr"][6] = (1 << 63) + 3
     ents["len"][7] = 0
+    ents["addr"][8] = (1 << 64) - 64  # addr + len wraps u64
+    ents["len"][8] = 64
+    ents["addr"][9] = (1 << 64) - 2048 + 16
     ring, mask = ring_of(ents, 8, 77)
     _check(cuda, g, o, umem, ring, mask, 77, len(ents), 0)
 
