@@ -7,24 +7,35 @@ header parse + 4-tuple demux) on MI355X.
 A "step" is one pass of the transform over one batch: BASELINE.json config 2
 (2^20 x 1514 B IPv4/UDP) per GPU by default.  Frames, descriptors and the
 filter tables are resident in HBM before the timed region; results (32 B per
-frame) are written to HBM.  For N > 1 (torchrun, one rank per GPU) every rank
-owns an independent shard of the packet stream (weak scaling, no data-path
-collective); the timed region is bracketed by a barrier + device sync, the
-max over ranks is taken, and rank 0 prints one JSON line.
+frame) are written to HBM.
+
+N > 1: one process per GPU.  Under torchrun (WORLD_SIZE set) --gpus must
+equal WORLD_SIZE; run directly, bench.py starts the N ranks itself (child
+processes, before anything touches a GPU) and exits with the worst rank's
+status.  Each rank owns a contiguous shard of the packet stream (weak
+scaling: N x the per-GPU packets; byte-balanced for the mixed-size configs,
+onload_amd/shards.py), rank 0 builds the filter tables and broadcasts the
+table image over RCCL, no collective touches the timed data path; the timed
+region is bracketed by a barrier + device sync, the max over ranks is taken,
+and rank 0 prints one JSON line (the records are then gathered to rank 0 and
+counted, outside the timed region).
 
 Extra objects on that line:
   roofline      algorithmic HBM bytes of one launch / its average duration
                 (HIP events on the launch stream) against the 8 TB/s peak;
                 traffic = PMC-measured HBM bytes per launch from
-                profiles/pmc_<config>.json when that file exists, else null.
-  cpu_baseline  the CPU oracle (the reference path restated in C, fixture
-                pinned) on host threads over the same frames (rank 0, N=1).
+                profiles/pmc_config<N>.json when that file exists, else null.
+  cpu_baseline  the CPU restatement of the reference path (fixture-pinned
+                oracle, a "port") on every host core this process may use,
+                over a bounded sample of the same frames (rank 0, N=1).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,14 +59,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main() -> None:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
     ap.add_argument("--n", type=int, default=0, help="packets per GPU (default: the config's)")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scatter", action="store_true",
                     help="N>1: also time an RCCL scatter of every shard from rank 0's GPU")
@@ -64,42 +75,107 @@ def main() -> None:
     ap.add_argument("--xdp", action="store_true",
                     help="also time the AF_XDP ring path (oo_gpu_rx_xdp_dev): the same frames in "
                          "a UMEM of 2048-B buffers at 256 B headroom, struct xdp_desc ring entries")
+    ap.add_argument("--xdp-host", action="store_true",
+                    help="also time zero-copy AF_XDP ingest: UMEM and ring in registered host "
+                         "memory read by the kernel over PCIe")
     ap.add_argument("--host-path", action="store_true",
-                    help="also time pinned H2D + transform + D2H (printed to stderr)")
-    args = ap.parse_args()
+                    help="also time the host-memory path: oo_gpu_rx_submit/_wait, pinned "
+                         "double-buffered H2D + transform + D2H")
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Start n ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, one GPU each) as child processes -- this process never
+    touches a GPU -- and return the worst exit status."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = c if rc == 0 else rc
+    return rc
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        if args.gpus > 1:
+            return launch_ranks(args.gpus, argv)
+    elif int(world_env) != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+        return 2
+    if os.environ.get("OO_BENCH_PROBE"):  # launcher test: report and stop before any GPU use
+        import torch
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")),
+                          "world": int(os.environ.get("WORLD_SIZE", "1")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "cuda_initialized": bool(torch.cuda.is_initialized())}), flush=True)
+        return 0
+    run_rank(args)
+    return 0
+
+
+def run_rank(args) -> None:
     import torch
     import torch.distributed as dist
+
+    from onload_amd import pktgen, shards
+    from onload_amd.rx import GpuRxStack
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    from onload_amd import pktgen
-    from onload_amd.rx import GpuRxStack
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     cfg = args.config
-    n = args.n or DEFAULT_N[cfg]
+    n_per = args.n or DEFAULT_N[cfg]
     seed = pktgen.default_seed(cfg)
+    n_total = n_per * world  # weak scaling
+    first, n = shards.shard_for(cfg, seed, n_total, rank, world)
     t0 = time.time()
     filters, socks = pktgen.world(cfg)
-    from shard import shard_range
-    first, _ = shard_range(n * world, rank, world)  # weak scaling: n per rank
     buf, desc = pktgen.generate(cfg, n, seed=seed, first=first)
-    log(f"[rank {rank}] generated {n} frames ({buf.nbytes / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] packets [{first}, {first + n}) ({buf.nbytes / 1e9:.2f} GB) "
+        f"generated in {time.time() - t0:.1f}s")
 
     stack = GpuRxStack(device=local)
-    stack.load_world(filters, socks)
-    frames = torch.from_numpy(buf).to(dev)
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
-    out = torch.empty(n * RESULT_B, dtype=torch.uint8, device=dev)
-    ctr = torch.zeros(32, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    table_bcast = None
+    if world > 1:
+        # Rank 0 owns the socket world; the others receive its table image.
+        if rank == 0:
+            stack.load_world(filters, socks)
+        dist.barrier()
+        tb = time.perf_counter()
+        nbytes = shards.broadcast_tables(stack, torch, dist, dev, 0, sh)
+        torch.cuda.synchronize(dev)
+        table_bcast = {"bytes": nbytes, "ms": round((time.perf_counter() - tb) * 1e3, 3)}
+    else:
+        stack.load_world(filters, socks)
+    frames = torch.from_numpy(buf).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    out = torch.empty(max(n, 1) * RESULT_B, dtype=torch.uint8, device=dev)
+    ctr = torch.zeros(32, dtype=torch.int32, device=dev)
     stack.sync(sh)
 
     def step():
@@ -132,20 +208,35 @@ def main() -> None:
     else:
         ms_step, kern_ms_max = local_ms, kern_ms
 
-    # Correctness of what was timed: counters of one more pass.
+    # What was timed is checked: one more pass with counters; N>1 gathers
+    # every rank's records to rank 0 (outside the timed region).
     stack.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
                               out.data_ptr(), ctr.data_ptr(), sh)
     torch.cuda.synchronize(dev)
+    gather = None
+    if world > 1:
+        dist.all_reduce(ctr)
+        tg = time.perf_counter()
+        recs = shards.gather_records(out, n, torch, dist, 0)
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            r = recs.view(-1, RESULT_B)[:, 0].cpu().numpy()
+            ok = bool((np.bincount(r, minlength=32) == ctr.cpu().numpy()).all())
+            gather = {"records": int(len(r)), "ms": round((time.perf_counter() - tg) * 1e3, 3),
+                      "counts_match": ok}
     counts = ctr.cpu().numpy()
-    assert counts.sum() == n, counts
+    assert counts.sum() == n_total, counts
 
-    mean_len = float(desc["len"].astype(np.float64).mean())
+    bytes_all = torch.tensor([float(buf.nbytes), float(desc["len"].astype(np.float64).sum())],
+                             dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(bytes_all)
+    mean_len = float(bytes_all[1]) / n_total
     alg_bytes_pkt = mean_len + DESC_B + RESULT_B
-    launch_bytes = alg_bytes_pkt * n
-    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9  # GB/s, this rank's kernel
-    total_pkts = n * world
-    mpps = total_pkts / (ms_step * 1e-3) / 1e6
-    gbs = total_pkts * alg_bytes_pkt / (ms_step * 1e-3) / 1e9
+    my_mean = float(desc["len"].astype(np.float64).mean()) if n else 0.0
+    achieved = (my_mean + DESC_B + RESULT_B) * n / (kern_ms * 1e-3) / 1e9  # this rank's kernel
+    mpps = n_total / (ms_step * 1e-3) / 1e6
+    gbs = n_total * alg_bytes_pkt / (ms_step * 1e-3) / 1e9
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json")
@@ -157,26 +248,28 @@ def main() -> None:
         except Exception:
             traffic = None
 
-    scatter = None
+    extras = {}
+    if table_bcast is not None:
+        extras["table_broadcast"] = table_bcast
+    if gather is not None:
+        extras["record_gather"] = gather
     if args.scatter and world > 1:
-        scatter = time_scatter(torch, dist, cfg, seed, n, rank, world, dev, buf)
-        if rank == 0:
-            log(f"[rank 0] rccl scatter: {json.dumps(scatter)}")
-
-    host_path = None
+        extras["rccl_scatter"] = time_scatter(torch, dist, shards, cfg, seed, n_total, rank,
+                                              world, dev, buf)
     if args.host_path:
-        host_path = time_host_path(torch, stack, buf, desc, dev)
-        log(f"[rank {rank}] host path: {json.dumps(host_path)}")
-
-    tx = None
+        extras["host_path"] = time_host_path(torch, filters, socks, buf, desc, local)
+        log(f"[rank {rank}] host path: {json.dumps(extras['host_path'])}")
     if args.tx:
-        tx = time_tx_fill(torch, stack, frames, d_desc, n, mean_len, sh, args.steps, args.warmup)
-        log(f"[rank {rank}] tx fill: {json.dumps(tx)}")
-
-    xdp = None
+        extras["tx_fill"] = time_tx_fill(torch, stack, frames, d_desc, n, my_mean, sh,
+                                         args.steps, args.warmup)
+        log(f"[rank {rank}] tx fill: {json.dumps(extras['tx_fill'])}")
     if args.xdp:
-        xdp = time_xdp(torch, stack, buf, desc, out, dev, sh, args.steps, args.warmup)
-        log(f"[rank {rank}] xdp ring: {json.dumps(xdp)}")
+        extras["xdp_ring"] = time_xdp(torch, stack, buf, desc, out, dev, sh, args.steps,
+                                      args.warmup)
+        log(f"[rank {rank}] xdp ring: {json.dumps(extras['xdp_ring'])}")
+    if args.xdp_host:
+        extras["xdp_host"] = time_xdp_host(torch, stack, buf, desc, out, dev, sh)
+        log(f"[rank {rank}] xdp host: {json.dumps(extras['xdp_host'])}")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -196,57 +289,51 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "u8/u16 integer (one's-complement sums in u32)",
             "data": "synthetic (seeded generator, onload_amd/csrc/oo_pktgen.c)",
-            "config": {"workload": WORKLOAD[cfg], "packets_per_gpu": n,
-                       "mean_frame_bytes": round(mean_len, 1), "sockets": len(socks),
-                       "filters": len(filters), "parallelism": f"shard{world}"},
+            "config": {"workload": WORKLOAD[cfg], "packets_per_gpu": n_per,
+                       "packets_total": n_total, "mean_frame_bytes": round(mean_len, 1),
+                       "sockets": len(socks), "filters": len(filters),
+                       "parallelism": f"shard{world}",
+                       "sharding": "bytes" if (world > 1 and cfg in shards.MIXED_CONFIGS)
+                       else "count"},
             "gbps": round(gbs, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 5),
                          "kernel_ms_max_rank": round(kern_ms_max, 5),
-                         "bytes_per_pkt": round(alg_bytes_pkt, 1)},
+                         "bytes_per_pkt": round(my_mean + DESC_B + RESULT_B, 1)},
             "cpu_baseline": cpu,
             "outcomes": {k: int(v) for k, v in enumerate(counts) if v},
         }
-        if host_path is not None:
-            line["host_path"] = host_path
-        if tx is not None:
-            line["tx_fill"] = tx
-        if xdp is not None:
-            line["xdp_ring"] = xdp
-        if scatter is not None:
-            line["rccl_scatter"] = scatter
+        line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def time_scatter(torch, dist, cfg, seed, n, rank, world, dev, my_buf, reps: int = 3):
+def time_scatter(torch, dist, shards, cfg, seed, n_total, rank, world, dev, my_buf,
+                 reps: int = 3):
     """Frames of all shards start on rank 0's GPU and are scattered over
-    RCCL/xGMI (one 16-B-padded slab per rank); timed on its own, outside the
+    RCCL/xGMI (one padded slab per rank); timed on its own, outside the
     device-resident metric.  Each rank checks it received its own shard."""
     from onload_amd import pktgen
-    from shard import shard_range
     size = torch.tensor([my_buf.nbytes], dtype=torch.int64, device=dev)
     dist.all_reduce(size, op=dist.ReduceOp.MAX)
     slab = int(size.item() + 15) // 16 * 16
-    recv = torch.empty(slab, dtype=torch.uint8, device=dev)
-    send = None
+    src = None
     if rank == 0:
-        send = []
+        src = []
         for r in range(world):
-            first, _ = shard_range(n * world, r, world)
-            b, _ = pktgen.generate(cfg, n, seed=seed, first=first)
-            t = torch.zeros(slab, dtype=torch.uint8, device=dev)
-            t[: b.nbytes] = torch.from_numpy(b).to(dev)
-            send.append(t)
+            f, c = shards.shard_for(cfg, seed, n_total, r, world)
+            b, _ = pktgen.generate(cfg, c, seed=seed, first=f)
+            src.append(torch.from_numpy(b).to(dev))
     times = []
+    recv = None
     for r in range(reps + 1):
         dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        dist.scatter(recv, send if rank == 0 else None, src=0)
+        recv = shards.scatter_frames(src, slab, torch, dist, dev, 0)
         torch.cuda.synchronize(dev)
         dist.barrier()
         if r:
@@ -282,19 +369,15 @@ def time_tx_fill(torch, stack, frames, d_desc, n, mean_len, sh, steps, warmup):
             "bytes_per_pkt": round(bpp, 1)}
 
 
-def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=256):
-    """The transform straight off an AF_XDP RX ring: the same frames laid out
-    as AF_XDP delivers them (each in its own 2048-B UMEM buffer at `headroom`,
-    a longer frame running on into the next buffers), the ring holding the
-    entries from a consumer index just below 2^32 so the ring and the u32
-    index both wrap.  Records must equal the descriptor path's (ref_out).
-    Algorithmic bytes as the main line's: frame + 16-B entry + 32-B record."""
-    from onload_amd import _abi
-    n = len(desc)
+def _umem_layout(buf, desc, headroom, out=None):
+    """The frames as AF_XDP delivers them: each in its own 2048-B buffer at
+    `headroom` (a longer frame running on into the next buffers).  Returns
+    (umem, entry addresses, lengths)."""
     lens = desc["len"].astype(np.int64)
     nch = (headroom + lens + 2047) // 2048
     addr = (np.concatenate(([0], np.cumsum(nch)[:-1])) * 2048 + headroom).astype(np.uint64)
-    umem = np.zeros(int(nch.sum()) * 2048, dtype=np.uint8)
+    size = int(nch.sum()) * 2048
+    umem = out[:size] if out is not None else np.zeros(size, dtype=np.uint8)
     offs = desc["frame_off"].astype(np.int64)
     for L in np.unique(lens):  # vectorised per frame length, in bounded pieces
         idx = np.nonzero(lens == L)[0]
@@ -303,21 +386,21 @@ def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=
         for i in range(0, len(idx), step):
             j = idx[i:i + step]
             umem[addr[j].astype(np.int64)[:, None] + col] = buf[offs[j][:, None] + col]
+    return umem, addr, lens
+
+
+def _ring(addr, lens, cons):
+    from onload_amd import _abi
+    n = len(addr)
     log2 = max(1, (n - 1).bit_length())
-    cons = (1 << 32) - n // 2
     ring = np.zeros(1 << log2, dtype=_abi.XDP_DESC_DTYPE)
     at = (cons + np.arange(n, dtype=np.uint64)) & np.uint64((1 << log2) - 1)
     ring["addr"][at] = addr
     ring["len"][at] = lens.astype(np.uint32)
-    d_umem = torch.from_numpy(umem).to(dev)
-    d_ring = torch.from_numpy(ring.view(np.uint8)).to(dev)
-    del umem
-    out = torch.empty_like(ref_out)
-    intf = int(desc["intf_i"][0]) if n else 0
+    return ring, (1 << log2) - 1
 
-    def run():
-        stack.xdp_dev(d_umem.data_ptr(), d_umem.numel(), d_ring.data_ptr(), (1 << log2) - 1,
-                      cons, n, intf, out.data_ptr(), 0, sh)
+
+def _timed(torch, run, steps, warmup):
     for _ in range(warmup):
         run()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -329,8 +412,30 @@ def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=
         run()
         e.record(stream)
     torch.cuda.synchronize()
+    return float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+
+def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=256):
+    """The transform straight off an AF_XDP RX ring in HBM: the same frames
+    in a UMEM of 2048-B buffers, the ring holding the entries from a consumer
+    index just below 2^32 so the ring and the u32 index both wrap.  Records
+    must equal the descriptor path's (ref_out).  Algorithmic bytes as the
+    main line's: frame + 16-B entry + 32-B record."""
+    n = len(desc)
+    umem, addr, lens = _umem_layout(buf, desc, headroom)
+    cons = (1 << 32) - n // 2
+    ring, mask = _ring(addr, lens, cons)
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_ring = torch.from_numpy(ring.view(np.uint8)).to(dev)
+    del umem
+    out = torch.empty_like(ref_out)
+    intf = int(desc["intf_i"][0]) if n else 0
+
+    def run():
+        stack.xdp_dev(d_umem.data_ptr(), d_umem.numel(), d_ring.data_ptr(), mask, cons, n, intf,
+                      out.data_ptr(), 0, sh)
+    ms = _timed(torch, run, steps, warmup)
     same = bool(torch.equal(out, ref_out)) and bool((desc["intf_i"] == intf).all())
-    ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     bpp = float(lens.mean()) + DESC_B + RESULT_B
     gbs = n * bpp / (ms * 1e-3) / 1e9
     return {"kernel_ms": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 1),
@@ -339,40 +444,101 @@ def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=
             "records_equal_descriptor_path": same}
 
 
-def time_host_path(torch, stack, buf, desc, dev, reps: int = 5):
-    """Pinned host frames -> H2D -> transform -> D2H results, one stream."""
+def _pinned_aligned(nbytes):
+    raw = np.zeros(nbytes + 8192, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    return raw[off:off + nbytes]
+
+
+def time_xdp_host(torch, stack, buf, desc, ref_out, dev, sh, reps=5, headroom=192):
+    """Zero-copy AF_XDP ingest: UMEM (chunk 2048,
+    headroom 192: tcp_helper_resource.c:137, 2205-2208) and ring in
+    registered host memory, read by the kernel in place over PCIe; records
+    must equal the descriptor path's.  Rate = frames per kernel time;
+    PCIe-bound (never `value`)."""
     n = len(desc)
-    h_frames = torch.from_numpy(buf).pin_memory()
-    h_desc = torch.from_numpy(desc.view(np.uint8)).pin_memory()
-    h_out = torch.empty(n * RESULT_B, dtype=torch.uint8).pin_memory()
-    d_frames = torch.empty_like(h_frames, device=dev)
-    d_desc = torch.empty_like(h_desc, device=dev)
-    d_out = torch.empty(n * RESULT_B, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    lens = desc["len"].astype(np.int64)
+    size = int(((headroom + lens + 2047) // 2048).sum()) * 2048
+    umem, addr, lens = _umem_layout(buf, desc, headroom, out=_pinned_aligned(size))
+    cons = (1 << 32) - 77
+    ring0, mask = _ring(addr, lens, cons)
+    ring = _pinned_aligned(ring0.nbytes).view(ring0.dtype)
+    ring[:] = ring0
+    d_umem = stack.host_register(umem)
+    d_ring = stack.host_register(ring)
+    out = torch.empty_like(ref_out)
+    intf = int(desc["intf_i"][0]) if n else 0
+
+    def run():
+        stack.xdp_dev(d_umem, umem.nbytes, d_ring, mask, cons, n, intf, out.data_ptr(), 0, sh)
+    ms = _timed(torch, run, reps, 1)
+    same = bool(torch.equal(out, ref_out))
+    stack.host_unregister(ring)
+    stack.host_unregister(umem)
+    frame_bytes = float(lens.sum())
+    return {"kernel_ms": round(ms, 3), "mpps": round(n / (ms * 1e-3) / 1e6, 2),
+            "pcie_GBps": round((frame_bytes + 16 * n) / (ms * 1e-3) / 1e9, 2),
+            "umem_bytes": int(umem.nbytes), "headroom": headroom,
+            "records_equal_descriptor_path": same}
+
+
+def time_host_path(torch, filters, socks, buf, desc, device, batch=1 << 16, reps=3):
+    """The path from host memory (NIC ring -> socket): frames and
+    descriptors in registered host memory, oo_gpu_rx_submit / _wait over
+    batches of `batch` packets, two in flight (H2D of one beside the
+    transform of the other), records landing in registered host memory.
+    Rate over the whole stream, PCIe-inclusive (never `value`)."""
+    from onload_amd import _abi
+    from onload_amd.rx import GpuRxStack
+    n = len(desc)
+    batch = min(batch, n)
+    starts = list(range(0, n, batch))
+    ends = [min(s + batch, n) for s in starts]
+    spans = [(int(desc["frame_off"][s]),
+              int(desc["frame_off"][e - 1]) + int(desc["len"][e - 1])) for s, e in zip(starts, ends)]
+    cap = max(b - a for a, b in spans)
+    hb = _pinned_aligned(buf.nbytes)
+    hb[:] = buf
+    hd = _pinned_aligned(desc.nbytes).view(_abi.DESC_DTYPE)
+    hd[:] = desc
+    for (s, e), (a, _) in zip(zip(starts, ends), spans):
+        hd["frame_off"][s:e] -= a  # each batch's offsets relative to its first frame
+    ho = _pinned_aligned(n * RESULT_B).view(_abi.RESULT_DTYPE)
+    g = GpuRxStack(device=device, host_stage_bytes=cap, host_stage_pkts=batch)
+    g.load_world(filters, socks)
+    for arr in (hb, hd, ho):
+        g.host_register(arr)
     times = []
     for r in range(reps + 1):
-        torch.cuda.synchronize(dev)
         t = time.perf_counter()
-        d_frames.copy_(h_frames, non_blocking=True)
-        d_desc.copy_(h_desc, non_blocking=True)
-        stack.handle_rx_batch_dev(d_frames.data_ptr(), d_frames.numel(), d_desc.data_ptr(), n,
-                                  d_out.data_ptr(), 0, stream.cuda_stream)
-        h_out.copy_(d_out, non_blocking=True)
-        torch.cuda.synchronize(dev)
+        pending = []
+        for (s, e), (a, b) in zip(zip(starts, ends), spans):
+            if len(pending) == 2:
+                g.wait(pending.pop(0))
+            pending.append(g.submit(hb[a:b], hd[s:e], ho[s:e]))
+        for tk in pending:
+            g.wait(tk)
         if r:
             times.append(time.perf_counter() - t)
     s = float(np.median(times))
     byt = buf.nbytes + desc.nbytes + n * RESULT_B
-    return {"mpps": round(n / s / 1e6, 2), "gbs_pcie": round(byt / s / 1e9, 2),
-            "ms": round(s * 1e3, 3)}
+    res = {"mpps": round(n / s / 1e6, 2), "gbs_pcie": round(byt / s / 1e9, 2),
+           "ms": round(s * 1e3, 3), "batch_pkts": batch, "in_flight": 2,
+           "registered": True}
+    for arr in (hb, hd, ho):
+        g.host_unregister(arr)
+    g.close()
+    return res
 
 
 def cpu_baseline(filters, socks, buf, desc, seconds):
-    """The oracle (reference CPU path restated in C, pinned by tests/golden)
-    on host threads over the same frames."""
+    """The CPU restatement of the reference path (oracle/rx_oracle.c, pinned
+    by tests/golden) on every host core this process may use, one thread per
+    core over contiguous shards of a bounded sample of the same frames."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from onload_amd.shards import host_cores
     from oracle_lib import OracleStack
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     o = OracleStack()
     o.load_world(filters, socks)
     sample = min(len(desc), 1 << 18)
@@ -387,9 +553,10 @@ def cpu_baseline(filters, socks, buf, desc, seconds):
             break
     return {"value": round(done / el / 1e6, 3), "unit": "Mpkt/s", "cores": threads,
             "kind": "port",
+            "label": f"Onload CPU-path semantics (restated, fixture-verified), {threads} cores",
             "sample": f"first {sample} frames of the same workload, repeated for {el:.1f}s "
                       f"({threads} threads, contiguous shards)"}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

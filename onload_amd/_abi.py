@@ -202,5 +202,8 @@ def load_pktgen(path: str = PKTGEN_PATH) -> ctypes.CDLL:
     lib.oo_pg_gen.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                               ctypes.c_int]
+    lib.oo_pg_split.restype = ctypes.c_int
+    lib.oo_pg_split.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
     _pg = lib
     return lib

@@ -476,3 +476,64 @@ uint64_t oo_pg_gen(int config, uint64_t seed, uint64_t first, uint32_t n,
   }
   return off;
 }
+
+/* Byte-balanced shard boundaries ("by cumulative bytes for
+ * IMIX/jumbo"): rank r owns packets [firsts[r], firsts[r+1]), where firsts[r]
+ * is the first packet whose packed bytes before it (at `align`) reach
+ * r / world of the total.  Two threaded passes over the lengths. */
+typedef struct {
+  int config; uint64_t seed, lo, hi; uint32_t align; uint64_t bytes;
+} split_job_t;
+
+static void* split_job(void* a)
+{
+  split_job_t* j = a;
+  uint64_t i, b = 0;
+  for( i = j->lo; i < j->hi; ++i )
+    b += (oo_pg_len(j->config, j->seed, i) + j->align - 1) / j->align * j->align;
+  j->bytes = b;
+  return NULL;
+}
+
+int oo_pg_split(int config, uint64_t seed, uint64_t n_total, int world, uint32_t align,
+                uint64_t* firsts, int nthreads)
+{
+  enum { MAXT = 64 };
+  pthread_t th[MAXT];
+  split_job_t jobs[MAXT];
+  uint64_t total = 0, before[MAXT + 1];
+  int t, r;
+  if( world < 1 || firsts == NULL ) return -1;
+  if( align == 0 ) align = 1;
+  if( nthreads < 1 ) nthreads = 1;
+  if( nthreads > MAXT ) nthreads = MAXT;
+  for( t = 0; t < nthreads; ++t ) {
+    jobs[t].config = config; jobs[t].seed = seed; jobs[t].align = align;
+    jobs[t].lo = n_total * (uint64_t)t / (uint64_t)nthreads;
+    jobs[t].hi = n_total * (uint64_t)(t + 1) / (uint64_t)nthreads;
+    pthread_create(&th[t], NULL, split_job, &jobs[t]);
+  }
+  for( t = 0; t < nthreads; ++t ) pthread_join(th[t], NULL);
+  for( t = 0; t < nthreads; ++t ) {
+    before[t] = total;
+    total += jobs[t].bytes;
+  }
+  before[nthreads] = total;
+  firsts[0] = 0;
+  firsts[world] = n_total;
+  for( r = 1; r < world; ++r ) {
+    /* the first packet whose bytes-before reach ceil(total * r / world) */
+    const uint64_t target = (total * (uint64_t)r + (uint64_t)world - 1) / (uint64_t)world;
+    uint64_t i, b;
+    t = 0;
+    while( t + 1 < nthreads && before[t + 1] < target ) ++t;
+    i = jobs[t].lo;
+    b = before[t];
+    while( i < n_total && b < target ) {
+      b += (oo_pg_len(config, seed, i) + align - 1) / align * align;
+      ++i;
+    }
+    firsts[r] = i < firsts[r - 1] ? firsts[r - 1] : i;
+  }
+  return 0;
+}

@@ -62,6 +62,11 @@ uint64_t oo_pg_gen(int config, uint64_t seed, uint64_t first, uint32_t n,
                    uint32_t align, uint8_t* buf, uint64_t cap,
                    oo_gpu_pkt_desc* desc, int nthreads);
 
+/* Byte-balanced shard boundaries of packets [0, n_total) over `world`
+ * ranks: firsts[0..world] (rank r owns [firsts[r], firsts[r+1])).  0 or -1. */
+int oo_pg_split(int config, uint64_t seed, uint64_t n_total, int world, uint32_t align,
+                uint64_t* firsts, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,17 +1,28 @@
 # SPDX-License-Identifier: BSD-2-Clause
-"""The N>1 path of bench.py on CPU (gloo, world_size 2): each rank owns an
-independent packet range (no data-path collective), outcomes aggregate by
-all_reduce, and the union of the shards equals one unsharded run."""
+"""The N>1 path of bench.py on CPU (gloo, world_size 2), through the same
+helpers the GPU run uses (onload_amd/shards.py):
+
+* shards: contiguous ranges covering the stream exactly, byte-balanced for
+  the mixed-size configurations;
+* the table image broadcast from rank 0 replicates its tables on rank 1;
+* per-rank records gathered to rank 0 equal one unsharded run, bit for bit;
+* the frame scatter delivers each rank its own shard;
+* bench.py --gpus N starts N ranks itself (WORLD_SIZE=N, before anything
+  initialises a GPU) and refuses a --gpus that disagrees with WORLD_SIZE."""
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from onload_amd import pktgen
-from shard import shard_range
+from onload_amd import pktgen, shards
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -26,19 +37,45 @@ def _worker(rank, world, port, config, n_total, q):
     import torch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from onload_amd.rx import GpuRxStack
     from oracle_lib import OracleStack, counters_of
-    first, n = shard_range(n_total, rank, world)
+    seed = pktgen.default_seed(config)
+    first, n = shards.shard_for(config, seed, n_total, rank, world)
     filters, socks = pktgen.world(config)
+    # tables: built on rank 0 only, replicated by the image broadcast
+    st = GpuRxStack(device=-1)
+    if rank == 0:
+        st.load_world(filters, socks)
+    shards.broadcast_tables(st, torch, dist, "cpu", 0)
+    img = torch.from_numpy(st.image_host())
+    ref = img.clone()
+    dist.broadcast(ref, src=0)
+    same_tables = bool(torch.equal(img, ref))
+    # records of this rank's shard, gathered to rank 0
     o = OracleStack()
     o.load_world(filters, socks)
     buf, desc = pktgen.generate(config, n, first=first, nthreads=2)
     res = o.handle_rx_batch(buf, desc)
     ctr = torch.from_numpy(counters_of(res).astype(np.int64))
     dist.all_reduce(ctr)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, res.tobytes())
+    recs = shards.gather_records(torch.from_numpy(res.view(np.uint8).copy()), n, torch, dist, 0)
+    # frames scattered from rank 0
+    slab = torch.tensor([buf.nbytes], dtype=torch.int64)
+    dist.all_reduce(slab, op=dist.ReduceOp.MAX)
+    src = None
     if rank == 0:
-        q.put((ctr.numpy(), b"".join(gathered)))
+        src = []
+        for r in range(world):
+            f, c = shards.shard_for(config, seed, n_total, r, world)
+            src.append(torch.from_numpy(pktgen.generate(config, c, first=f, nthreads=2)[0]))
+    got = shards.scatter_frames(src, int(slab.item()), torch, dist, "cpu", 0)
+    scatter_ok = torch.tensor([int(np.array_equal(got[: buf.nbytes].numpy(), buf))])
+    dist.all_reduce(scatter_ok, op=dist.ReduceOp.MIN)
+    tables_ok = torch.tensor([int(same_tables)])
+    dist.all_reduce(tables_ok, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        q.put((ctr.numpy(), recs.numpy().tobytes(), int(scatter_ok.item()),
+               int(tables_ok.item()), img.numpy().tobytes()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -52,12 +89,17 @@ def test_two_rank_shards_equal_one_run(config):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, config, n_total, q)) for r in range(2)]
     for p in procs:
         p.start()
-    ctr, recs = q.get(timeout=120)
+    ctr, recs, scatter_ok, tables_ok, img = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    assert scatter_ok == 1 and tables_ok == 1
+    from onload_amd.rx import GpuRxStack
     from oracle_lib import OracleStack, counters_of
     filters, socks = pktgen.world(config)
+    st = GpuRxStack(device=-1)
+    st.load_world(filters, socks)
+    assert img == st.image_host().tobytes()  # rank 1's replica is rank 0's tables
     o = OracleStack()
     o.load_world(filters, socks)
     buf, desc = pktgen.generate(config, n_total, nthreads=2)
@@ -69,8 +111,52 @@ def test_two_rank_shards_equal_one_run(config):
 def test_shard_ranges_cover_exactly():
     for n in (0, 1, 7, 1 << 20, 12345):
         for w in (1, 2, 3, 8):
-            spans = [shard_range(n, r, w) for r in range(w)]
+            spans = [shards.shard_range(n, r, w) for r in range(w)]
             assert spans[0][0] == 0
             assert sum(s[1] for s in spans) == n
             for a, b in zip(spans, spans[1:]):
                 assert a[0] + a[1] == b[0]
+
+
+@pytest.mark.parametrize("config,n_total,world", [(5, 200000, 8), (4, 50000, 3), (5, 17, 4)])
+def test_byte_balanced_shards(config, n_total, world):
+    """Mixed-size traffic: contiguous ranges, equal packed bytes within one
+    frame's worth."""
+    seed = pktgen.default_seed(config)
+    spans = shards.split_bytes(config, seed, n_total, world)
+    assert spans[0][0] == 0 and sum(c for _, c in spans) == n_total
+    for a, b in zip(spans, spans[1:]):
+        assert a[0] + a[1] == b[0]
+    per = [pktgen.nbytes(config, seed, f, c) for f, c in spans]
+    total = pktgen.nbytes(config, seed, 0, n_total)
+    assert sum(per) == total
+    if n_total > 1000:
+        assert max(per) - min(per) <= 2 * 9088, per  # within about one jumbo frame
+        # count-split would be far less even for config 4 / 5
+        counts = [pktgen.nbytes(config, seed, *shards.shard_range(n_total, r, world))
+                  for r in range(world)]
+        assert max(per) - min(per) <= max(counts) - min(counts)
+
+
+def _bench(args, env):
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                          capture_output=True, text=True, env=env, timeout=300)
+
+
+def test_bench_launches_ranks_before_gpu_use():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OO_BENCH_PROBE"] = "1"
+    r = _bench(["--gpus", "3", "--steps", "1"], env)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == [0, 1, 2]
+    assert all(x["world"] == 3 and x["local_rank"] == x["rank"] for x in lines)
+    assert not any(x["cuda_initialized"] for x in lines)
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", OO_BENCH_PROBE="1")
+    r = _bench(["--gpus", "4"], env)
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr
