@@ -885,13 +885,16 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
   // Static balanced partition: the W waves each take K = ceil(n / (64 W))
   // tiles; NT = W K tiles of tlo or tlo + 8 packets (multiples of 8, at most
-  // 64), the last taking the < 8 left over.  Small batches use fewer blocks.
+  // 64), the last taking the < 8 left over.  Small batches use fewer blocks
+  // (and fewer tiles than waves when n < 8 W: no tile is empty).
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full
   const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
   const uint64_t K = (n + 64 * W - 1) / (64 * W);
-  const uint64_t NT = W * K;
+  // W K tiles, but never an empty one (every tile holds at least 8 packets,
+  // or the whole batch): waves past the last tile have none.
+  const uint64_t NT = std::max<uint64_t>(1, std::min<uint64_t>(W * K, n / 8));
   const uint64_t step = c->tstep;
   const uint64_t tlo = std::min<uint64_t>(64 - step, (n / NT) / step * step);
   P.ntiles = (uint32_t)NT;

@@ -24,7 +24,7 @@
 //     header sum, the L4 sum inside the window, handle_rx_pkt's
 //     frag/options/TCP-scattered tests and the 2 or 3 lookup stages --
 //     giving a 32-B record that is final unless the L4 region runs past the
-//     window (parse_packet);
+//     window (parse_headers, demux_packet);
 //   * the body: the frame bytes past the window, summed by 8-lane groups
 //     (128 contiguous bytes per group per round, one packet per group at a
 //     time) from a ring of 1-KiB LDS-DMA pieces (Body).  Only the
@@ -229,85 +229,179 @@ __device__ __forceinline__ bool bind2dev_ok(const KParams& P, uint32_t sflags, u
   return hw < 64 && (hwports & (1ull << hw)) != 0 && b2d_vlan == vlan;
 }
 
-__device__ __forceinline__ Slot4 load_slot4(const KParams& P, uint32_t i) {
-  const uint4* p = reinterpret_cast<const uint4*>(P.slot4 + i);
-  Slot4 r;
-  uint4* d = reinterpret_cast<uint4*>(&r);
-  d[0] = p[0];
-  d[1] = p[1];
-  return r;
+// A slot record as loaded: an IPv4 Slot4 in d0..d1, an IPv6 Slot6 in
+// d0..d3 (oo_rx_device.h).
+struct Rec {
+  uint4 d0, d1, d2, d3;
+};
+
+// The table a lane probes.  One wave may hold IPv4 and IPv6 packets; each
+// lane walks its own table in the same instruction stream (one chain of
+// dependent loads per wave, not one per address family).  The table
+// addresses are picked from the (scalar) kernel arguments at each use: held
+// per lane they would be loop-invariant VGPRs the kernel cannot afford.
+struct Probe {
+  uint64_t occ, slots;  // this lane's table (per tile: not loop-invariant)
+  uint32_t mask;
+  bool is6;
+};
+
+// A kernel-argument value forced into a scalar register: a per-lane select
+// between two kernel-argument fields may otherwise be turned into a vector
+// load from the argument segment (a memory round trip and a vmcnt(0) drain).
+__device__ __forceinline__ uint32_t sreg(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
-__device__ __forceinline__ Slot6 load_slot6(const KParams& P, uint32_t i) {
-  const uint4* p = reinterpret_cast<const uint4*>(P.slot6 + i);
-  Slot6 r;
-  uint4* d = reinterpret_cast<uint4*>(&r);
-  d[0] = p[0];
-  d[1] = p[1];
-  d[2] = p[2];
-  d[3] = p[3];
-  return r;
+__device__ __forceinline__ uint64_t sreg64(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  return (uint64_t)sreg((uint32_t)v) | ((uint64_t)sreg((uint32_t)(v >> 32)) << 32);
 }
 
-// ci_netif_filter_for_each_match (netif_table.c:234-319) over the slot
-// records, every match counted.  The caller has loaded the not-EMPTY bits of
-// the first slot (occ) and of the next one on the probe sequence (occ_next),
-// and the first slot's record when occ: the common walk (an EMPTY first
-// slot, or one occupied slot followed by an EMPTY one) needs no more loads.
-__device__ Match walk4(const KParams& P, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
-                       uint32_t proto, int intf_i, int vlan, uint32_t h1, uint32_t h2, bool occ,
-                       Slot4 rec, bool occ_next) {
-  Match m = {-1, 0};
-  const uint32_t mask = P.ip4_mask;
-  const uint32_t first = h1;
-  bool check_lport = false;  // the first slot's lport is implied (LPRP, hash.h:76-163)
-  for (uint32_t guard = 0; guard <= mask; ++guard) {
-    if (!occ) break;  // an EMPTY slot ends the walk
-    const uint32_t st = rec.id_state & ST_MASK;
-    if ((check_lport ? occupied(st) : st == ST_PREFERRED) && rec.laddr == la &&
-        rec.raddr == ra && rec.rport == rp && rec.proto == proto &&
-        (!check_lport || rec.lport == lp) &&
-        bind2dev_ok(P, rec.sflags, rec.hwports, rec.b2d_vlan, intf_i, vlan)) {
-      if (m.n == 0) m.first = (int32_t)(rec.id_state & ID_MASK);
-      ++m.n;
-    }
-    h1 = (h1 + h2) & mask;
-    if (h1 == first) break;
-    occ = guard == 0 ? occ_next : occ_bit(P.occ4, h1);
-    if (occ) rec = load_slot4(P, h1);
-    check_lport = true;
+// Global-address-space loads from an address held as an integer (a plain
+// pointer rebuilt from one would be a flat access, counted in lgkmcnt too).
+typedef const __attribute__((address_space(1))) uint32_t* g_cu32p;
+typedef const __attribute__((address_space(1))) u32x4* g_cu32x4p;
+__device__ __forceinline__ uint32_t gload4(uint64_t a) { return *reinterpret_cast<g_cu32p>(a); }
+__device__ __forceinline__ uint4 gload16(uint64_t a) {
+  const u32x4 v = *reinterpret_cast<g_cu32x4p>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// A 64-bit per-lane choice between two scalar values, as two 32-bit
+// selects (a 64-bit select may become a divergent branch that splits a batch
+// of loads).
+__device__ __forceinline__ uint64_t sel64(bool c, uint64_t a, uint64_t b) {
+  const uint32_t lo = c ? (uint32_t)a : (uint32_t)b, hi = c ? (uint32_t)(a >> 32) : (uint32_t)(b >> 32);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+__device__ __forceinline__ Probe probe_of(const KParams& P, bool is6) {
+  Probe t;
+  t.is6 = is6;
+  t.mask = is6 ? sreg(P.ip6_mask) : sreg(P.ip4_mask);
+  t.occ = sel64(is6, sreg64(P.occ6), sreg64(P.occ4));
+  t.slots = sel64(is6, sreg64(P.slot6), sreg64(P.slot4));
+  return t;
+}
+
+// The occupancy words of six slots (every stage's first slot and its
+// successor) in one batch: six loads, one wait.  Written as one asm block
+// because the register-bound scheduler otherwise consumes each load before
+// issuing the next (six memory latencies instead of one).  The wait is
+// vmcnt(0): loads complete in issue order and these are the newest, so it
+// waits for nothing they would not.
+__device__ __forceinline__ void occ_words6(const Probe& t, const uint32_t i[6], uint32_t w[6]) {
+  uint64_t a[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) a[k] = t.occ + 4u * (i[k] >> 5);
+  asm volatile(
+      "global_load_dword %0, %6, off\n\tglobal_load_dword %1, %7, off\n\t"
+      "global_load_dword %2, %8, off\n\tglobal_load_dword %3, %9, off\n\t"
+      "global_load_dword %4, %10, off\n\tglobal_load_dword %5, %11, off\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5])
+      : "memory");
+}
+
+__device__ __forceinline__ bool probe_occ(const KParams& P, const Probe& t, uint32_t i) {
+  (void)P;
+  return ((gload4(t.occ + 4u * (i >> 5)) >> (i & 31u)) & 1u) != 0;
+}
+
+__device__ __forceinline__ Rec load_rec(const KParams& P, const Probe& t, uint32_t i, bool any6) {
+  (void)P;
+  const uint64_t a = t.slots + ((uint64_t)i << (t.is6 ? 6 : 5));
+  Rec r;
+  r.d0 = gload16(a);
+  r.d1 = gload16(a + 16u);
+  r.d2 = r.d3 = make_uint4(0, 0, 0, 0);
+  if (any6 && t.is6) {
+    r.d2 = gload16(a + 32u);
+    r.d3 = gload16(a + 48u);
   }
-  return m;
+  return r;
 }
 
+// One visited slot against the lookup key:
+//  IPv4 (handle_entry, netif_table.c:192-231): the first probe matches only
+//   an OCCUPIED_PREFERRED entry and its lport is implied (LPRP, hash.h:76-163,
+//   :280); later probes match any occupied entry with lport compared;
+//   laddr, raddr, rport and protocol always (raddr/rport/protocol are the
+//   socket's, ip.h:1315-1340).
+//  IPv6 (netif_table_ip6.c:146-170): occupied (id >= 0), laddr, lport,
+//   protocol, and either raddr/rport or -- for a wildcard lookup -- a socket
+//   that is not connected.
+// Then ci_sock_intf_check.  *id is the entry's socket id.
+template <bool IS6>
+__device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool first4,
+                                          const uint32_t la[4], uint32_t lp, const uint32_t ra[4],
+                                          bool ra_null, uint32_t rp, uint32_t proto, int intf_i,
+                                          int vlan, int32_t& id) {
+  bool ok;
+  uint32_t sflags;
+  int b2d;
+  uint64_t hw;
+  if (!IS6) {
+    const uint32_t st = r.d0.x & ST_MASK;
+    ok = (first4 ? st == ST_PREFERRED : (occupied(st) && (r.d0.w & 0xffffu) == lp)) &&
+         r.d0.y == la[0] && r.d0.z == ra[0] && (r.d0.w >> 16) == rp && (r.d1.x & 0xffu) == proto;
+    sflags = r.d1.x >> 16;
+    b2d = (int)(int16_t)(r.d1.y & 0xffffu);
+    hw = (uint64_t)r.d1.z | ((uint64_t)r.d1.w << 32);
+    id = (int32_t)(r.d0.x & ID_MASK);
+  } else {
+    id = (int32_t)r.d0.x;
+    sflags = r.d2.w >> 16;
+    ok = id >= 0 && r.d0.z == la[0] && r.d0.w == la[1] && r.d1.x == la[2] && r.d1.y == la[3] &&
+         (r.d2.z & 0xffffu) == lp && (r.d2.w & 0xffu) == proto &&
+         (ra_null ? !(sflags & OO_GPU_RX_SOCK_CONNECTED)
+                  : (r.d1.z == ra[0] && r.d1.w == ra[1] && r.d2.x == ra[2] && r.d2.y == ra[3] &&
+                     (r.d2.z >> 16) == rp));
+    b2d = (int)(int16_t)(r.d3.x & 0xffffu);
+    hw = (uint64_t)r.d3.z | ((uint64_t)r.d3.w << 32);
+  }
+  return ok && bind2dev_ok(P, sflags, hw, b2d, intf_i, vlan);
+}
+
+// ci_netif_filter_for_each_match (netif_table.c:234-319) /
 // ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189) over the
-// slot records; same first-slot convention as walk4.
-__device__ Match walk6(const KParams& P, const uint32_t la[4], uint32_t lp, const uint32_t ra[4],
-                       bool ra_null, uint32_t rp, uint32_t proto, int intf_i, int vlan,
-                       uint32_t h1, uint32_t h2, bool occ, Slot6 rec, bool occ_next) {
+// slot records, every match counted.  The caller has loaded the not-EMPTY
+// bits of the first slot (occ) and of the next one on the probe sequence
+// (occ_next), and -- when have -- the first slot's record: the common walk
+// (an EMPTY first slot, or one occupied slot followed by an EMPTY one) needs
+// no more loads.  Tombstones continue the walk; an EMPTY slot or a full
+// cycle ends it.
+template <bool IS6>
+__device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_t la[4],
+                      uint32_t lp, const uint32_t ra[4], bool ra_null, uint32_t rp, uint32_t proto,
+                      int intf_i, int vlan, uint32_t h1, uint32_t h2, bool occ, Rec rec, bool have,
+                      bool occ_next) {
   Match m = {-1, 0};
-  const uint32_t mask = P.ip6_mask;
   const uint32_t first = h1;
-  for (uint32_t guard = 0; guard <= mask; ++guard) {
-    if (!occ) break;  // an EMPTY slot ends the walk (tombstones continue)
-    if (rec.id >= 0 && rec.laddr[0] == la[0] && rec.laddr[1] == la[1] &&
-        rec.laddr[2] == la[2] && rec.laddr[3] == la[3] && rec.lport == lp &&
-        rec.proto == proto &&
-        (ra_null ? !(rec.sflags & OO_GPU_RX_SOCK_CONNECTED)
-                 : (rec.raddr[0] == ra[0] && rec.raddr[1] == ra[1] && rec.raddr[2] == ra[2] &&
-                    rec.raddr[3] == ra[3] && rec.rport == rp)) &&
-        bind2dev_ok(P, rec.sflags, rec.hwports, rec.b2d_vlan, intf_i, vlan)) {
-      if (m.n == 0) m.first = rec.id;
+  if (occ && !have) rec = load_rec(P, t, h1, any6);  // the first slot's record was not preloaded
+  for (uint32_t guard = 0; guard <= t.mask; ++guard) {
+    if (!occ) break;  // an EMPTY slot ends the walk
+    int32_t id;
+    if (rec_match<IS6>(P, rec, guard == 0, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id)) {
+      if (m.n == 0) m.first = id;
       ++m.n;
     }
-    h1 = (h1 + h2) & mask;
+    h1 = (h1 + h2) & t.mask;
     if (h1 == first) break;
-    occ = guard == 0 ? occ_next : occ_bit(P.occ6, h1);
-    if (occ) rec = load_slot6(P, h1);
+    if (guard == 0) {
+      occ = occ_next;
+      if (occ) rec = load_rec(P, t, h1, any6);
+    } else {
+      // Deeper in a chain: the record is loaded beside its occupancy bit
+      // (one load latency per step, not two; an EMPTY slot's record is
+      // simply not used).
+      rec = load_rec(P, t, h1, any6);
+      occ = probe_occ(P, t, h1);
+    }
   }
   return m;
 }
-
-
 
 // ---------------------------------------------------------------------------
 // Header work of one packet (one lane).
@@ -371,6 +465,17 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
   auto BE16 = [&](int j) -> uint32_t { return (B(j) << 8) | B(j + 1); };
   auto N16 = [&](int j) -> uint32_t { return B(j) | (B(j + 1) << 8); };
   auto N32 = [&](int j) -> uint32_t { return N16(j) | (N16(j + 2) << 16); };
+  // Window bytes j .. j+3 as a little-endian word, unmasked (two aligned
+  // 4-B LDS reads inside the window).
+  auto D4 = [&](int j) -> uint32_t {
+    int w = shift + j;
+    w = w < HB - 4 ? w : HB - 4;
+    const int d = w >> 2;
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(W.cell(d >> 2) + 4 * (d & 3));
+    const int e = d + 1 < HB / 4 ? d + 1 : d;
+    const uint32_t hi = *reinterpret_cast<const uint32_t*>(W.cell(e >> 2) + 4 * (e & 3));
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(w & 3));
+  };
 
   Hdr h;
   h.flags = 0;
@@ -519,15 +624,24 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
         late = OO_RX_R_IP4_FRAG;  // netif_event.c:293-295
       } else if (ihl4 > 20) {
         // ci_ip_options_parse (netif_event.c:135-185), signed-char lengths.
+        // Four option bytes per step: a run of NOPs at the front is taken
+        // whole (a run that reaches the end of the options ends the walk,
+        // as the byte-at-a-time loop would), else one option.  Bytes read at
+        // or past `end` only ever end the walk, so they need no masking.
         int o = l3 + 20;
         const int end = l3 + ihl4;
         bool err = false;
-        while (B(o) != 0u && o < end && !err) {
-          const uint32_t kind = B(o);
-          if (kind == 1u) {
-            ++o;
+        while (o < end && !err) {
+          const uint32_t b4 = D4(o);
+          const uint32_t kind = b4 & 0xffu;
+          if (kind == 0u) break;  // IPOPT_EOL
+          if (kind == 1u) {       // IPOPT_NOP run: count the leading 0x01 bytes
+            const uint32_t x = b4 ^ 0x01010101u;
+            const uint32_t nz = (x & 0xffu ? 1u : 0u) | (x & 0xff00u ? 2u : 0u) |
+                                (x & 0xff0000u ? 4u : 0u) | (x & 0xff000000u ? 8u : 0u);
+            o += nz ? (int)__builtin_ctz(nz) : 4;
           } else if (kind == 7u || kind == 68u || kind == 130u || kind == 136u) {
-            const int l = (int)(int8_t)(uint8_t)B(o + 1);
+            const int l = (int)(int8_t)(uint8_t)(b4 >> 8);
             if (l < 4 || l > end - o) err = true;
             else o += l;
           } else {
@@ -705,10 +819,10 @@ __device__ __forceinline__ void read_cells(const Win& W, uint4 (&c)[HC]) {
       : "memory");
 }
 
-// handle_rx_pkt + the lookup stages (netif_event.c:250-451) for one packet
-// (one lane), from its header fields.
-__device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, int shift,
-                                               int len, int intf_i, uint64_t abase, int span) {
+// The header stage of one packet (one lane): the fixed-format paths when
+// they apply, the general walk otherwise (handle_rx_csum_bad's gates and
+// checksums, handle_rx_pkt's IPv4 checks).
+__device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, uint64_t abase) {
   const int off0 = (int)body_off0(abase);
   Hdr h;
   bool fixed;
@@ -725,6 +839,47 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, i
   if (__ballot(!fixed) != 0) {
     if (!fixed) h = parse_general(W, shift, len, off0);
   }
+  return h;
+}
+
+// The 2 (UDP) or 3 (TCP) lookup stages of one lane in reference order; the
+// first stage with a match decides (*stage = 1..3).
+template <bool IS6>
+__device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t, bool any6,
+                                               const Hdr& h, uint32_t dport, uint32_t sport,
+                                               uint32_t proto, int intf_i, int vlan, bool tcp,
+                                               uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
+                                               bool o0, bool o1, bool o2, bool q0, bool q1,
+                                               bool q2, Rec rec, int fs, int& stage) {
+  const uint32_t zero[4] = {0, 0, 0, 0};
+  const uint32_t dx = IS6 ? (h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3]) : h.da[0];
+  const uint32_t sx = IS6 ? (h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3]) : h.sa[0];
+  Match m = walk<IS6>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
+                      hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0);
+  stage = 1;
+  if (m.n == 0) {
+    m = walk<IS6>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
+                  hash2(dx, dport, 0u, 0u, proto), o1, rec, fs == 1, q1);
+    stage = 2;
+  }
+  if (m.n == 0 && tcp) {
+    m = walk<IS6>(P, t, any6, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2,
+                  hash2(0u, dport, 0u, 0u, proto), o2, rec, fs == 2, q2);
+    stage = 3;
+  }
+  return m;
+}
+
+// The record of one packet from its headers: the lookup stages of
+// ci_udp_handle_rx (udp_rx.c:271-306: full 4-tuple, then (laddr, lport)) or
+// ci_tcp_handle_rx (tcp_rx.c:4786-4835: then (*, lport)); the first stage
+// with a match decides.  IPv4 and IPv6 lanes share one instruction stream:
+// every stage's first-slot and next-slot occupancy bits are loaded together,
+// then the first slots' records, so a wave pays two dependent loads however
+// its packets mix address families and protocols.
+template <bool ANY6>
+__device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h, int intf_i,
+                                                 uint64_t abase, int span, int shift) {
   const int vlan = (int)h.vlan;
   const uint32_t proto = h.proto;
   uint32_t reason = h.reason;
@@ -739,12 +894,13 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, i
     r.proto = (uint8_t)proto;
     r.ip_paylen = (uint16_t)h.ip_paylen;
   }
+  // Lanes that reach the lookups.
+  bool look = false;
   if (reason == PENDING) {
     flags |= OO_RX_F_CSUM_OK;
     r.l4_off = (uint16_t)h.l4;
-    const uint32_t sport = h.sport, dport = h.dport;
-    r.sport_be = (uint16_t)sport;
-    r.dport_be = (uint16_t)dport;
+    r.sport_be = (uint16_t)h.sport;
+    r.dport_be = (uint16_t)h.dport;
     if (is6) {
       r.saddr_be = h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3];
       r.daddr_be = h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3];
@@ -753,12 +909,44 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, i
       r.daddr_be = h.da[0];
     }
     reason = h.late;
-
-    if (reason == PENDING) {
-      // Demux stages in reference order (udp_rx.c:271-306,
-      // tcp_rx.c:4786-4835); the first stage with a match decides.  The
-      // first probe of every stage is loaded up front.
-      r.hash3 = hash3(r.daddr_be, dport, r.saddr_be, sport, proto);
+    look = reason == PENDING;
+  }
+  if (__ballot(look) != 0) {
+    constexpr bool any6 = ANY6;
+    const uint32_t sport = h.sport, dport = h.dport;
+    const uint32_t dx = r.daddr_be, sx = r.saddr_be;  // hash addresses
+    const Probe t = probe_of(P, ANY6 && is6);
+    const bool tcp = proto == 6u;
+    const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & t.mask;
+    const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & t.mask;
+    const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & t.mask;
+    const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
+    const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
+    const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
+    // All six bits in one batch (a UDP lane's stage-3 bits are unused).
+    bool o0 = false, o1 = false, o2 = false, q0 = false, q1 = false, q2 = false;
+    if (look) {
+      const uint32_t idx[6] = {h1_0, h1_1, h1_2, (h1_0 + h2_0) & t.mask, (h1_1 + h2_1) & t.mask,
+                               (h1_2 + h2_2) & t.mask};
+      uint32_t w[6];
+      occ_words6(t, idx, w);
+      auto bit = [&](int k) { return ((w[k] >> (idx[k] & 31u)) & 1u) != 0; };
+      o0 = bit(0);
+      o1 = bit(1);
+      o2 = bit(2) && tcp;
+      q0 = bit(3);
+      q1 = bit(4);
+      q2 = bit(5) && tcp;
+    }
+    // One record per lane up front: the first slot of the first stage whose
+    // first slot is occupied (a stage with an EMPTY first slot ends at once,
+    // and that record usually decides); a later stage loads its own only
+    // when this one did not match.
+    const int fs = o0 ? 0 : o1 ? 1 : o2 ? 2 : 3;
+    Rec rec = {};
+    if (look && fs < 3) rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
+    if (look) {
+      r.hash3 = hash3(dx, dport, sx, sport, proto);
       if (proto == 17u) {
         // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
         // of the L3 header (udp_rx.c:157-159): bytes 16..19, which for
@@ -766,72 +954,15 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, i
         const uint32_t dd = is6 ? h.sa[2] : h.da[0];
         if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
       }
-      const int nst = proto == 6u ? 3 : 2;
-      Match m = {-1, 0};
-      int stage = 0;
-      // Every stage's first slot bit, its successor's bit and the first
-      // slot's record are loaded up front (two dependent levels; loading the
-      // records unconditionally, one level, was slower: the 2-MiB record
-      // array does not stay in L2 beside the stream); the walks then
-      // usually need nothing more.
-      if (is6) {
-        const uint32_t zero[4] = {0, 0, 0, 0};
-        const uint32_t dx = r.daddr_be, sx = r.saddr_be;
-        const uint32_t mask = P.ip6_mask;
-        const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & mask;
-        const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & mask;
-        const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
-        const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
-        const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
-        const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
-        const bool o0 = occ_bit(P.occ6, h1_0), o1 = occ_bit(P.occ6, h1_1);
-        const bool o2 = nst == 3 && occ_bit(P.occ6, h1_2);
-        const bool q0 = occ_bit(P.occ6, (h1_0 + h2_0) & mask);
-        const bool q1 = occ_bit(P.occ6, (h1_1 + h2_1) & mask);
-        const bool q2 = nst == 3 && occ_bit(P.occ6, (h1_2 + h2_2) & mask);
-        Slot6 s0 = {}, s1 = {}, s2 = {};
-        if (o0) s0 = load_slot6(P, h1_0);
-        if (o1) s1 = load_slot6(P, h1_1);
-        if (o2) s2 = load_slot6(P, h1_2);
-        m = walk6(P, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
-        stage = 1;
-        if (m.n == 0) {
-          m = walk6(P, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
-          stage = 2;
-        }
-        if (m.n == 0 && nst == 3) {
-          m = walk6(P, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
-          stage = 3;
-        }
-      } else {
-        const uint32_t da = r.daddr_be, sa = r.saddr_be;
-        const uint32_t mask = P.ip4_mask;
-        const uint32_t h1_0 = hash3(da, dport, sa, sport, proto) & mask;
-        const uint32_t h1_1 = hash3(da, dport, 0u, 0u, proto) & mask;
-        const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & mask;
-        const uint32_t h2_0 = hash2(da, dport, sa, sport, proto);
-        const uint32_t h2_1 = hash2(da, dport, 0u, 0u, proto);
-        const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
-        const bool o0 = occ_bit(P.occ4, h1_0), o1 = occ_bit(P.occ4, h1_1);
-        const bool o2 = nst == 3 && occ_bit(P.occ4, h1_2);
-        const bool q0 = occ_bit(P.occ4, (h1_0 + h2_0) & mask);
-        const bool q1 = occ_bit(P.occ4, (h1_1 + h2_1) & mask);
-        const bool q2 = nst == 3 && occ_bit(P.occ4, (h1_2 + h2_2) & mask);
-        Slot4 s0 = {}, s1 = {}, s2 = {};
-        if (o0) s0 = load_slot4(P, h1_0);
-        if (o1) s1 = load_slot4(P, h1_1);
-        if (o2) s2 = load_slot4(P, h1_2);
-        m = walk4(P, da, dport, sa, sport, proto, intf_i, vlan, h1_0, h2_0, o0, s0, q0);
-        stage = 1;
-        if (m.n == 0) {
-          m = walk4(P, da, dport, 0u, 0u, proto, intf_i, vlan, h1_1, h2_1, o1, s1, q1);
-          stage = 2;
-        }
-        if (m.n == 0 && nst == 3) {
-          m = walk4(P, 0u, dport, 0u, 0u, proto, intf_i, vlan, h1_2, h2_2, o2, s2, q2);
-          stage = 3;
-        }
-      }
+      // The walks compare per address family (divergent only in waves that
+      // hold both): the loads above were shared.
+      Match m;
+      int stage;
+      if (ANY6 && is6) m = lookup_stages<true>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp,
+                                               h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs,
+                                               stage);
+      else m = lookup_stages<false>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0,
+                                    h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
       reason = OO_RX_R_NO_MATCH;
       if (m.n) {
         reason = OO_RX_R_DELIVER;
@@ -853,6 +984,15 @@ __device__ __forceinline__ Parsed parse_packet(const KParams& P, const Win& W, i
   if (h.longl4 && h.E4 < span) ps.s4 -= window_sum_global(abase, h.E4, span);
   ps.odd_long = (uint32_t)(shift & 1) | (h.longl4 ? 2u : 0u);
   return ps;
+}
+
+// A wave whose lookups are all IPv4 takes the IPv4-only instance (the
+// IPv6 compares and record halves compiled out).
+__device__ __forceinline__ Parsed demux_packet(const KParams& P, const Hdr& h, int intf_i,
+                                               uint64_t abase, int span, int shift) {
+  if (__ballot(h.is6 && h.reason == PENDING && h.late == PENDING) != 0)
+    return demux_packet_t<true>(P, h, intf_i, abase, span, shift);
+  return demux_packet_t<false>(P, h, intf_i, abase, span, shift);
 }
 
 // The verdict a long packet's record waited for: the window part plus the
@@ -899,9 +1039,22 @@ struct Jobs {       // a tile's jobs: lane (g, j) holds job q = g + 8 j
   uint32_t T;       // rounds of the tile
 };
 
+// max(v) over lanes lane ^ 8, lane ^ 16 and lane ^ 32 (the lanes with the
+// same lane & 7) -- DPP, swizzle and permlane32_swap: no address VGPRs (a
+// per-lane bpermute address is a loop-invariant VGPR the kernel would spill).
+__device__ __forceinline__ uint32_t max_x8(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
+  v = max(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401f));  // lane ^ 16
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // lane ^ 32
+  return max((uint32_t)p[0], (uint32_t)p[1]);
+}
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) v = max(v, lane_get(v, lane ^ d));
+  (void)lane;
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));   // [1,0,3,2]
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));   // [2,3,0,1]
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // half mirror
+  v = max_x8(v);
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
@@ -949,12 +1102,8 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
   J.nb = lane_get(nb, jp);
   J.lim = lane_get((uint32_t)span - off0, jp);
   // R_j: the most rounds over lanes 8g + j
-  uint32_t m = (J.nb + 7u) >> 3;
-  m = max(m, lane_get(m, lane ^ 8u));
-  m = max(m, lane_get(m, lane ^ 16u));
-  m = max(m, lane_get(m, lane ^ 32u));
-  J.rj = m;
-  J.T = (uint32_t)__builtin_amdgcn_readlane((int)group_sum8(m), 0);
+  J.rj = max_x8((J.nb + 7u) >> 3);
+  J.T = (uint32_t)__builtin_amdgcn_readlane((int)group_sum8(J.rj), 0);
   return J;
 }
 
@@ -1367,15 +1516,27 @@ __device__ __forceinline__ void lds_write16(void* p, const uint4& v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(w) : "memory");
 }
 
-// The wave's NST_TX = 8 stores.  Frames in the whole-granule form (TxHdr):
+// The wave's NST_TX = 6 stores (tests/test_kernel_isa.py checks the code
+// object holds exactly these).  Frames in the whole-granule form (TxHdr):
 // their first 64 B with the check fields patched in (fixed format: IPv4
 // check at 24, UDP at 40, TCP at 50), staged through the idle ring so that
 // store u writes the granules of frames 16u .. 16u + 15, four lanes per
 // granule -- whole 64-B writes.  Every other frame: the two check fields as
-// byte stores (little-endian, as the reference's u16 stores).  Lanes with
-// nothing to write store to the sink, so the count is static.  All lanes
-// active; the ring holds no DMA (the body stream has drained).
-constexpr int NST_TX = 8;
+// 16-bit stores (little-endian, as the reference's u16 stores; the address
+// may be odd).  Lanes with nothing to write store to the sink, so the count
+// is static.  All stores are global-address-space (a flat store would count
+// in lgkmcnt too).  All lanes active; the ring holds no DMA (the body stream
+// has drained).
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) uint16_t g_uint16;
+__device__ __forceinline__ void gstore16(uint64_t a, const uint4& v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  *reinterpret_cast<g_u32x4*>(a) = w;
+}
+__device__ __forceinline__ void gstore2(uint64_t a, uint32_t v) {
+  *reinterpret_cast<g_uint16*>(a) = (uint16_t)v;
+}
+constexpr int NST_TX = 6;
 static_assert(R >= 4, "store_checks stages 64 lanes x 64 B in the ring");
 __device__ __forceinline__ void store_checks(const KParams& P, const DescView& dv,
                                              const TxHdr& h, uint32_t l4v, uint32_t lane,
@@ -1408,17 +1569,13 @@ __device__ __forceinline__ void store_checks(const KParams& P, const DescView& d
       const bool wf = lane_get(whole ? 1u : 0u, f) != 0;
       const uint64_t a = (uint64_t)lane_get((uint32_t)fa, f) |
                          ((uint64_t)lane_get((uint32_t)(fa >> 32), f) << 32);
-      uint4* const dst = wf ? reinterpret_cast<uint4*>(a) + (lane & 3u)
-                            : reinterpret_cast<uint4*>(P.sink) + lane;
-      *dst = v;
+      gstore16(wf ? a + 16u * (lane & 3u) : reinterpret_cast<uint64_t>(P.sink) + 16u * lane, v);
     }
   }
   uint8_t* const pi = ip ? frame + h.ip_pos : sink;
   uint8_t* const pl = l4 ? frame + h.l4_pos : sink + 2;
-  pi[0] = (uint8_t)h.ip_ck;
-  pi[1] = (uint8_t)(h.ip_ck >> 8);
-  pl[0] = (uint8_t)l4v;
-  pl[1] = (uint8_t)(l4v >> 8);
+  gstore2(reinterpret_cast<uint64_t>(pi), h.ip_ck);
+  gstore2(reinterpret_cast<uint64_t>(pl), l4v);
 }
 
 // ---------------------------------------------------------------------------
@@ -1485,15 +1642,20 @@ __device__ __forceinline__ void vm_wait_n(int n) {
 // The tile's records (packet p's in lane p): the wave writes them as two
 // contiguous 1-KiB runs, store u taking records 32u .. 32u + 31 with lane L
 // writing half L & 1 of record 32u + L / 2 -- whole lines per instruction,
-// not 16 B at a 32-B stride.  Records past the tile's count go to the sink,
-// so the wave always issues exactly NST stores.  All lanes active.
+// not 16 B at a 32-B stride.  Lanes past the tile's count write the tile's
+// last record again (the same bytes to the same address), so the wave always
+// issues exactly NST stores and needs no per-lane sink address (tiles are
+// never empty: the host's partition, oo_gpu_rx.cpp launch()).  All lanes
+// active.
 __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
                                               const oo_gpu_rx_result& r, uint32_t lane) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
-  const bool hi = (lane & 1u) != 0;
+  const uint32_t hi = lane & 1u;
+  const uint32_t last = t.cnt - 1u;
+  uint4* const out = reinterpret_cast<uint4*>(P.out);
 #pragma unroll
   for (uint32_t u = 0; u < 2; ++u) {
-    const uint32_t q = 32u * u + (lane >> 1);
+    const uint32_t q = min(32u * u + (lane >> 1), last);
     uint4 v;
     uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
 #pragma unroll
@@ -1501,9 +1663,7 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
       const uint32_t a = lane_get(w[d], q), b = lane_get(w[4 + d], q);
       vw[d] = hi ? b : a;
     }
-    uint4* o = q < t.cnt ? reinterpret_cast<uint4*>(P.out + t.first + q)
-                         : reinterpret_cast<uint4*>(P.sink) + 2u * q;
-    o[hi ? 1 : 0] = v;
+    out[(size_t)(t.first + q) * 2u + hi] = v;
   }
 }
 
@@ -1558,8 +1718,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 #endif
     IssueCursor ci;
     issue_slot(ci, J, 0, lane, zero);
-    ConsumeCursor cc;
-    consume_start(cc, J, lane);
     // This tile's header windows: older than the previous tile's NST stores
     // (none before the first tile) and the R rounds issued here.
     if (T != 0) {
@@ -1584,8 +1742,9 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       ps = Parsed{};
       ps.r.reason = (uint8_t)(lds_read16(&L.hdr[0][lane]).x & 7u);
 #else
-      ps = parse_packet(P, window_of(L.hdr, lane), dv.shift, dv.len, dv.intf_i, dv.abase,
-                        dv.span);
+      const Hdr h = parse_headers(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
+      STAMP(2, __builtin_amdgcn_s_memrealtime());
+      ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
 #endif
     }
     STAMP(3, __builtin_amdgcn_s_memrealtime());
@@ -1602,6 +1761,11 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       (void)dn;
 #endif
     }
+
+    // The consume side's cursor is set up only now: its registers are free
+    // during the header work, where the demux loads need them.
+    ConsumeCursor cc;
+    consume_start(cc, J, lane);
 
     // ---- body stream (T is a multiple of R), two pieces per step.  Pieces
     // newer than the awaited pair: the rest of the ring, plus the NHS

@@ -1,0 +1,75 @@
+# SPDX-License-Identifier: BSD-2-Clause
+"""Static checks on the gfx950 code object that the kernels' counted
+`s_waitcnt vmcnt(N)` waits rely on (oo_rx_kernel.hip "rx_kernel"):
+
+* no scratch: a spill or stack object adds vector-memory operations the
+  counts do not know about (they only make a wait stricter, but each costs a
+  drain on the stream), so the kernels must stay within their VGPR budget;
+* the stores per tile are exactly the ones the counts assume: rx_kernel two
+  16-B record stores (NST), tx_kernel four 16-B granule stores plus two
+  16-bit check-field stores (NST_TX), all global (a flat store counts in
+  lgkmcnt too) -- a compiler that merged or split stores would make the
+  waits too loose (round 1's byte stores were in fact merged).
+
+Compiles the kernel source to assembly with hipcc (cross-compiles, no GPU)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "onload_amd", "csrc", "oo_rx_kernel.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("isa") / "k.s"
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950",
+                        "--offload-device-only", "-S", "-o", str(out), SRC,
+                        "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True, check=True)
+    return out.read_text(), r.stderr
+
+
+def _body(text, name):
+    m = re.search(rf"^{name}:.*?^\.Lfunc_end", text, re.S | re.M)
+    assert m, name
+    return m.group(0)
+
+
+def _usage(stderr, mangled):
+    i = stderr.index(f"Function Name: {mangled}")
+    block = stderr[i:i + 2000]
+    get = lambda k: int(re.search(rf"{k}: (\d+)", block).group(1))  # noqa: E731
+    return {k: get(k) for k in ("VGPRs", "ScratchSize \\[bytes/lane\\]", "VGPRs Spill")}
+
+
+@pytest.mark.parametrize("kernel", ["_ZN5oo_rx9rx_kernelENS_7KParamsE",
+                                    "_ZN5oo_rx9tx_kernelENS_7KParamsE"])
+def test_no_scratch(asm, kernel):
+    text, stderr = asm
+    u = _usage(stderr, kernel)
+    assert u["VGPRs Spill"] == 0, u
+    # no scratch access in the kernel or the (rare-path) function it calls; the
+    # reported ScratchSize may still hold a call frame reservation
+    assert "scratch_" not in _body(text, kernel)
+    assert "scratch_" not in _body(text, "_ZN5oo_rx17window_sum_globalEmii")
+    assert u["VGPRs"] <= 168, u  # 3 waves per SIMD (amdgpu_waves_per_eu(3))
+
+
+def test_store_counts(asm):
+    text, _ = asm
+    rx = _body(text, "_ZN5oo_rx9rx_kernelENS_7KParamsE")
+    # store_records: two 16-B stores per tile (NST)
+    assert len(re.findall(r"global_store_dwordx4", rx)) == 2
+    assert not re.findall(r"global_store_(byte|short|dword\b|dwordx2)", rx)
+    tx = _body(text, "_ZN5oo_rx9tx_kernelENS_7KParamsE")
+    assert len(re.findall(r"global_store_short\b", tx)) == 2
+    assert len(re.findall(r"global_store_dwordx4", tx)) == 4
+    assert not re.findall(r"global_store_(byte|dword\b|dwordx2)", tx)
+    for body in (rx, tx):  # flat stores would count in lgkmcnt as well
+        assert not re.findall(r"flat_store|flat_load|flat_atomic", body)

@@ -9,7 +9,8 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 T=$(mktemp -d)
 git -C "$ROOT" archive "$REV" onload_amd/csrc include | tar -x -C "$T"
 mkdir -p "$ROOT/build"
+SRCS=$(ls "$T"/onload_amd/csrc/*.hip "$T"/onload_amd/csrc/oo_gpu_rx.cpp "$T"/onload_amd/csrc/oo_rx_csum.cpp 2>/dev/null)
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -shared \
-  -o "$ROOT/build/var_$NAME.so" "$T/onload_amd/csrc/oo_rx_kernel.hip" "$T/onload_amd/csrc/oo_gpu_rx.cpp"
+  -o "$ROOT/build/var_$NAME.so" $SRCS
 rm -rf "$T"
 echo "build/var_$NAME.so <- $REV"

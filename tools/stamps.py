@@ -78,7 +78,8 @@ def main() -> None:
         "wave_end_us_pct": [float(np.percentile(rows[:, 2], q) / 1e3) for q in (0, 10, 50, 90, 100)],
         "wave_start_us_max": float(rows[:, 3].max() / 1e3),
         "per_tile_us_mean": {
-            "hdr_wait": float(d(0, 1).mean() / 1e3), "parse_demux": float(d(1, 3).mean() / 1e3),
+            "hdr_wait": float(d(0, 1).mean() / 1e3), "parse": float(d(1, 2).mean() / 1e3),
+            "demux": float(d(2, 3).mean() / 1e3),
             "stream": float(d(3, 4).mean() / 1e3),
             "record": float(d(4, 5).mean() / 1e3), "total": float(d(0, 5).mean() / 1e3),
             "gap_to_next": float(np.mean([(a[w, i + 1, 0] - a[w, i, 5]) * ns
