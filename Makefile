@@ -9,14 +9,20 @@ CFLAGS   ?= -O2 -std=gnu11 -fPIC -Wall -Wextra -Wno-unused-parameter
 
 PRODUCT := onload_amd/liboo_gpu_rx.so
 PKTGEN  := onload_amd/liboo_pktgen.so
+SHIM    := onload_amd/liboo_rx_poll.so
 SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_table_kernel.hip \
            onload_amd/csrc/oo_gpu_rx.cpp onload_amd/csrc/oo_rx_csum.cpp
 HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 
-all: $(PRODUCT) $(PKTGEN) oracle tools/hbm_ceiling
+all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling
 
 $(PRODUCT): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,liboo_gpu_rx.so -o $@ $(SRCS)
+
+# The batched ci_netif_poll_evq RX branch (plain C over the C ABI).
+$(SHIM): src/shim/oo_rx_poll.c include/oo_rx_poll.h include/oo_gpu_rx.h $(PRODUCT)
+	$(CC) $(CFLAGS) -Iinclude -shared -o $@ src/shim/oo_rx_poll.c \
+	  -Lonload_amd -l:liboo_gpu_rx.so -Wl,-rpath,'$$ORIGIN'
 
 $(PKTGEN): onload_amd/csrc/oo_pktgen.c onload_amd/csrc/oo_pktgen.h include/oo_gpu_rx.h
 	$(CC) $(CFLAGS) -shared -o $@ onload_amd/csrc/oo_pktgen.c -lm -lpthread
@@ -35,13 +41,24 @@ VARIANTS ?= sp4:-DOO_RX_SP=4 sp8:-DOO_RX_SP=8
 variants: $(SRCS) $(HDRS)
 	mkdir -p build
 	for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo "$${v#*:}" | tr ',' ' '); \
-	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/var_$$n.so $(SRCS) || exit 1; done
+	  $(HIPCC) $(HIPFLAGS) $$f -shared -Wl,-soname,liboo_gpu_rx.so -o build/var_$$n.so $(SRCS) || exit 1; done
 
 clean:
-	rm -f $(PRODUCT) $(PKTGEN)
+	rm -f $(PRODUCT) $(SHIM) $(PKTGEN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean variants
+# Check-only: the ci_netif_poll_evq integration (integration/netif_event_gpu.c)
+# compiled against the reference tree's own sources and headers (this
+# container only; never shipped).
+REF ?= /root/reference
+check-integration: oracle
+	mkdir -p build
+	$(CC) -c -O2 -Wall -Werror '-DTRANSPORT_CONFIG_OPT_HDR=<ci/internal/transport_config_opt_cloud.h>' \
+	  -Ioracle/_ref -I$(REF)/src/include -I$(REF)/src/lib/transport/ip \
+	  -I$(REF)/src/lib/transport/common -I$(REF)/src/lib/ciul -I$(REF)/src/lib/citools \
+	  -Iinclude -o build/netif_event_gpu.o integration/netif_event_gpu.c
+
+.PHONY: all oracle asm clean variants check-integration
 
 tools/hbm_ceiling: tools/hbm_ceiling.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<

@@ -518,6 +518,40 @@ int oo_or_slot(const oo_or_tables* t, int af, uint32_t slot,
   return -EINVAL;
 }
 
+/* Every slot that differs from its initial state, as rows of six int64
+ * {af, slot, a, b, c, d}: IPv4 {id_state, laddr, route_count, lport}, IPv6
+ * {id, route_count, laddr[0..7], laddr[8..15]} (little-endian halves) -- the
+ * dump format of the table fixtures (tests/golden/make_table_golden.py).
+ * Returns the number of rows (rows may be NULL to count). */
+uint32_t oo_or_dump(const oo_or_tables* t, int64_t* rows, uint32_t cap)
+{
+  uint32_t i, n = 0;
+  for( i = 0; i <= t->ip4_mask; ++i )
+    if( t->ip4_id_state[i] != ST_EMPTY || t->ip4_laddr[i] || t->ip4_route[i] ||
+        t->ip4_lport[i] ) {
+      if( rows && n < cap ) {
+        int64_t* r = rows + 6 * (size_t)n;
+        r[0] = 4; r[1] = i; r[2] = t->ip4_id_state[i]; r[3] = t->ip4_laddr[i];
+        r[4] = t->ip4_route[i]; r[5] = t->ip4_lport[i];
+      }
+      ++n;
+    }
+  for( i = 0; i <= t->ip6_mask; ++i ) {
+    const ip6e_t* e = &t->ip6[i];
+    int64_t lo, hi;
+    memcpy(&lo, e->laddr, 8);
+    memcpy(&hi, e->laddr + 8, 8);
+    if( e->id != ID6_EMPTY || e->route_count || lo || hi ) {
+      if( rows && n < cap ) {
+        int64_t* r = rows + 6 * (size_t)n;
+        r[0] = 6; r[1] = i; r[2] = e->id; r[3] = e->route_count; r[4] = lo; r[5] = hi;
+      }
+      ++n;
+    }
+  }
+  return n;
+}
+
 /* ------------------------------------------------------------------ */
 /* Demux walks: count every match of one stage, remember the first.     */
 

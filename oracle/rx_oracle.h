@@ -35,6 +35,7 @@ int  oo_or_lookup(const oo_or_tables* t, int af, const void* laddr,
 int  oo_or_slot(const oo_or_tables* t, int af, uint32_t slot,
                 uint32_t* id_state, int32_t* route_count, uint16_t* lport);
 int  oo_or_sock_set(oo_or_tables* t, int32_t id, const oo_gpu_rx_sock* s);
+uint32_t oo_or_dump(const oo_or_tables* t, int64_t* rows, uint32_t cap);
 
 /* One frame: the whole handle_rx_csum_bad -> handle_rx_pkt -> L4 demux. */
 void oo_or_rx_one(const oo_or_tables* t, const uint8_t* frame, int len,

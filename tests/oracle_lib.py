@@ -40,6 +40,7 @@ def oracle():
             "oo_or_slot": (ctypes.c_int, [_P, ctypes.c_int, _U32, ctypes.POINTER(_U32),
                                           ctypes.POINTER(_I32), ctypes.POINTER(_U16)]),
             "oo_or_sock_set": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_abi.Sock)]),
+            "oo_or_dump": (_U32, [_P, _P, _U32]),
             "oo_or_rx_one": (None, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
             "oo_or_rx_batch": (None, [_P, _P, ctypes.c_uint64, _P, _U32, _P, ctypes.c_int]),
             "oo_or_ip4_hdr_ok": (ctypes.c_int, [_P, ctypes.c_int]),
@@ -148,6 +149,13 @@ class OracleStack:
 
     def sock_set(self, sock_id, sock):
         return self._lib.oo_or_sock_set(self._t, sock_id, ctypes.byref(sock))
+
+    def dump(self) -> np.ndarray:
+        """Sparse table rows (af, slot, a, b, c, d) as the table fixtures hold them."""
+        n = self._lib.oo_or_dump(self._t, None, 0)
+        rows = np.zeros((n, 6), dtype=np.int64)
+        self._lib.oo_or_dump(self._t, rows.ctypes.data, n)
+        return rows
 
     def load_world(self, filters, socks):
         for i, s in enumerate(socks):
