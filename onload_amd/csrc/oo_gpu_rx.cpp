@@ -95,6 +95,8 @@ static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
 constexpr int NTRACK = 8;             // streams whose last launch is tracked
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
+constexpr uint32_t CLAIM_SLOTS = 16;  // tile-claim counter sets (launches in flight)
+constexpr uint32_t CLAIM_GROUPS = 64; // wave groups per launch at most (128 B each)
 
 // The last launch on one stream (cross-stream ordering of table changes).
 struct Tracked {
@@ -163,6 +165,11 @@ struct oo_gpu_rx_ctx {
   Tracked track[NTRACK];
   uint64_t lru = 0;
   uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros + the sink
+  uint32_t* d_claim = nullptr; // CLAIM_SLOTS x CLAIM_GROUPS counter pairs, 128 B apart
+  uint32_t claim_seq = 0;      // launches so far (picks the pair)
+  bool dyn = true;             // dynamic tile claims (OO_RX_STATIC=1: static)
+  uint32_t tail_tile = 32;     // packets per tile at the batch's end (dynamic)
+  uint32_t tail_per_wave = 1;  // such tiles per wave
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t tstep = 8;          // tile size step (KParams::tstep)
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
@@ -446,7 +453,7 @@ void mirror_from_image(oo_gpu_rx_ctx* c, const uint8_t* src) {
 void free_dev(oo_gpu_rx_ctx* c) {
   DevTables& T = c->T;
   for (void* p : {(void*)T.slot4, (void*)T.rc4, (void*)T.occ4, (void*)T.slot6, (void*)T.occ6,
-                  (void*)T.socks, (void*)T.sockgen, (void*)c->d_zero})
+                  (void*)T.socks, (void*)T.sockgen, (void*)c->d_zero, (void*)c->d_claim})
     if (p) (void)hipFree(p);
   for (OpStage& st : c->stage) {
     if (st.h) (void)hipHostFree(st.h);
@@ -635,6 +642,9 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       c->grid = std::max<uint32_t>(1, (uint32_t)(b0 * prop.multiProcessorCount) * pct / 100);
   }
   c->tstep = env_u32("OO_RX_TSTEP", 8) == 1 ? 1 : 8;
+  c->dyn = env_u32("OO_RX_STATIC", 0) == 0;
+  c->tail_tile = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_TAIL_TILE", 32) / 8 * 8));
+  c->tail_per_wave = env_u32("OO_RX_TAIL_PER_WAVE", 1);
   DevTables& T = c->T;
   T.ip4_mask = c->ip4_mask;
   T.ip6_mask = c->ip6_mask;
@@ -651,6 +661,8 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       hipMalloc(&T.socks, sizeof(oo_gpu_rx_sock) * c->max_socks) == hipSuccess &&
       hipMalloc(&T.sockgen, sizeof(uint32_t) * c->max_socks) == hipSuccess &&
       hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + 64u * 32u) == hipSuccess &&
+      hipMalloc(&c->d_claim, 128u * CLAIM_SLOTS * CLAIM_GROUPS) == hipSuccess &&
+      hipMemsetAsync(c->d_claim, 0, 128u * CLAIM_SLOTS * CLAIM_GROUPS, c->stream) == hipSuccess &&
       hipHostMalloc(&c->h_image_hdr, sizeof(ImageHdr), hipHostMallocDefault) == hipSuccess &&
       hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
       oo_table_launch_init(&T, c->stream) == 0;
@@ -883,24 +895,51 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
   P.stamps = c->stamps;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
-  // Static balanced partition: the W waves each take K = ceil(n / (64 W))
-  // tiles; NT = W K tiles of tlo or tlo + 8 packets (multiples of 8, at most
-  // 64), the last taking the < 8 left over.  Small batches use fewer blocks
-  // (and fewer tiles than waves when n < 8 W: no tile is empty).
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full
   const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
-  const uint64_t K = (n + 64 * W - 1) / (64 * W);
-  // W K tiles, but never an empty one (every tile holds at least 8 packets,
-  // or the whole batch): waves past the last tile have none.
-  const uint64_t NT = std::max<uint64_t>(1, std::min<uint64_t>(W * K, n / 8));
-  const uint64_t step = c->tstep;
-  const uint64_t tlo = std::min<uint64_t>(64 - step, (n / NT) / step * step);
-  P.ntiles = (uint32_t)NT;
-  P.tlo = (uint32_t)tlo;
-  P.ta = (uint32_t)std::min<uint64_t>(NT, (n - tlo * NT) / step);
-  P.tstep = (uint32_t)step;
+  // The launch's claim counters (zero: every launch leaves them reset), one
+  // pair per wave group: the largest power of two <= CLAIM_GROUPS dividing W.
+  P.claim = c->d_claim + 32u * CLAIM_GROUPS * (c->claim_seq++ % CLAIM_SLOTS);
+  P.ngroups = 1;
+  while (P.ngroups < CLAIM_GROUPS && W % (2u * P.ngroups) == 0) P.ngroups *= 2;
+  P.dyn = c->dyn ? 1u : 0u;
+  if (c->dyn) {
+    // Dynamic: full 64-packet tiles, then about tail_per_wave tiles of
+    // tail_tile packets per wave (the last taking what is left, at least
+    // one packet), so the waves that finish early take the small tiles and
+    // all end within a small tile of each other.
+    const uint64_t S = c->tail_tile;
+    const uint64_t tail = W * c->tail_per_wave * S;
+    const uint64_t NA = n > tail ? (n - tail) / 64 : 0;
+    const uint64_t NS = S < 64 ? (n - 64 * NA + S - 1) / S : 0;
+    P.ntiles = (uint32_t)(NA + NS);
+    P.tlo = (uint32_t)S;
+    P.tstep = (uint32_t)(64 - S);
+    P.ta = (uint32_t)NA;
+    if (S == 64) {  // no tail: plain 64-packet tiles
+      P.ntiles = (uint32_t)((n + 63) / 64);
+      P.tlo = 64;
+      P.tstep = 0;
+      P.ta = 0;
+    }
+  } else {
+    // Static balanced partition: the W waves each take K = ceil(n / (64 W))
+    // tiles; NT = W K tiles of tlo or tlo + 8 packets (multiples of 8, at
+    // most 64), the last taking the < 8 left over.  Small batches use fewer
+    // blocks (and fewer tiles than waves when n < 8 W: no tile is empty).
+    const uint64_t K = (n + 64 * W - 1) / (64 * W);
+    // W K tiles, but never an empty one (every tile holds at least 8
+    // packets, or the whole batch): waves past the last tile have none.
+    const uint64_t NT = std::max<uint64_t>(1, std::min<uint64_t>(W * K, n / 8));
+    const uint64_t step = c->tstep;
+    const uint64_t tlo = std::min<uint64_t>(64 - step, (n / NT) / step * step);
+    P.ntiles = (uint32_t)NT;
+    P.tlo = (uint32_t)tlo;
+    P.ta = (uint32_t)std::min<uint64_t>(NT, (n - tlo * NT) / step);
+    P.tstep = (uint32_t)step;
+  }
   const int grid = (int)blocks;
   const int rc = tx ? oo_tx_launch(&P, grid, s) : oo_rx_launch(&P, grid, s);
   if (rc != 0) return -EIO;

@@ -177,12 +177,12 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
 }
 
 #ifdef OO_RX_STAMPS
-// Diagnostic phase stamps: stamps[((wave * 64 + iter) * 8) + phase] = realtime
-// (100 MHz) for the first 64 tiles of each wave.
+// Diagnostic phase stamps: stamps[((wave * 128 + iter) * 8) + phase] = realtime
+// (100 MHz) for the first 128 tiles of each wave.
 #define STAMP(ph, val)                                                                \
   do {                                                                                \
-    if (P.stamps != nullptr && lane == 0 && it_ < 64)                                \
-      P.stamps[((size_t)gwave * 64 + it_) * 8 + (ph)] = (val);                        \
+    if (P.stamps != nullptr && lane == 0 && it_ < 128)                               \
+      P.stamps[((size_t)gwave * 128 + it_) * 8 + (ph)] = (val);                       \
   } while (0)
 #else
 #define STAMP(ph, val) \
@@ -1584,26 +1584,46 @@ __device__ __forceinline__ void store_checks(const KParams& P, const DescView& d
 // descriptors of the tile after it) land in LDS, so each tile starts with its
 // headers in place.  A wave's vector-memory operations (loads, LDS-DMA,
 // stores) retire in issue order, and every wait counts the operations issued
-// after the ones it needs: NHS staging operations per tile (HC header rows and
-// one descriptor line) and NST record stores, both issued by the whole
-// wave whatever its lanes hold, so the counts are static.
+// after the ones it needs: NHS staging operations per tile (HC header rows,
+// one descriptor line and the tile claim) and NST record stores, all issued
+// by the wave whatever its lanes hold, so the counts are static.
+//
+// Tiles are handed out dynamically: a wave's first three tiles are gwave +
+// k W (k < 3), every later one comes from a counter (claim_tile), claimed
+// three tiles ahead -- the descriptors are prefetched two tiles ahead -- so
+// a wave that runs fast takes more tiles and the waves finish together (the
+// host cuts the batch's end into small tiles, launch()).  Atomics on one
+// address serialise (~12 ns each), so the waves are split into P.ngroups
+// groups of W / ngroups waves (gwave mod ngroups, spread over all CUs), each
+// with its own counter over its own tiles (those = its group mod ngroups).
+// The last wave of a group to finish resets the group's counters for the
+// launch that reuses them.
 
 #ifdef OO_RX_ABL_NOHDR
-constexpr int NHS = 1;
+constexpr int NHS = 2;
 #else
-constexpr int NHS = HC + 1;
+constexpr int NHS = HC + 2;
 #endif
 #ifdef OO_RX_ABL_NOSTORE
 constexpr int NST = 0;
 #else
 constexpr int NST = 2;
 #endif
+// Extra body rounds a long tile puts in flight in the header rows once the
+// parse has read them (the header work then overlaps E more KiB of stream).
+#ifndef OO_RX_EXTRA
+#define OO_RX_EXTRA 8
+#endif
+constexpr int E = OO_RX_EXTRA;
+static_assert(E % 2 == 0 && E <= HC, "extra rounds live in the header rows");
 
 struct WaveLds {
   uint4 hdr[HC][64];            // header windows (stage_window)
   uint4 ring[R][64];            // body ring: slot = one round of the eight groups
   uint4 desc[2][64];            // descriptors of this tile and of the next
   uint32_t cnt[OO_RX_R_COUNT];  // per-reason counts
+  uint32_t dbase, gofs;          // claims: first dynamic tile of the group, counter offset
+  uint32_t T0, pad;              // the tile's body rounds (kept out of the registers)
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
 constexpr int WAVE_U4 = (int)(sizeof(WaveLds) / 16);
@@ -1667,6 +1687,15 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
   }
 }
 
+// One tile claim: lane 0 adds 1 to the launch's counter and gets the old
+// value back in `got` (one returning global atomic: one vector-memory
+// operation of the wave, counted like the others).  The compiler tracks the
+// result and waits for it where it is read, a tile later.
+__device__ __forceinline__ void claim_tile(uint32_t* ctr, uint32_t step, uint32_t lane,
+                                           uint32_t& got) {
+  if (lane == 0) got = __hip_atomic_fetch_add(ctr, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The per-wave tile loop of rx_kernel (TX = false) and tx_kernel (TX =
 // true): the same staging and body stream, different header work and stores.
 template <bool TX>
@@ -1680,18 +1709,25 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   const uint32_t lane = threadIdx.x & 63u;
   WaveLds& L = reinterpret_cast<WaveLds*>(smem)[wave];
 
-  const uint32_t gwave = blockIdx.x * WAVES + wave;
+  const uint32_t gwave = sreg(blockIdx.x * WAVES + wave);  // wave-uniform
   const uint32_t W = gridDim.x * WAVES;
-  const uint32_t K = (P.ntiles - gwave + W - 1) / W;  // this wave's tiles gwave + k W
-  if (gwave >= P.ntiles) return;
+  // Tiles i, i + 1, i + 2 of this wave, and the claim of tile i + 3.
+  uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
+  // Group g's claims are g + 3 W, g + 3 W + ngroups, ... (its counter holds
+  // the multiple of ngroups handed out); kept in LDS, out of the registers.
+  if (lane == 0) {
+    lds_write4(&L.dbase, 3u * W + (gwave & (P.ngroups - 1u)));
+    lds_write4(&L.gofs, 32u * (gwave & (P.ngroups - 1u)));
+  }
+  if (gwave < P.ntiles) {
   if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
 
   // Prologue: this tile's descriptors, then the next tile's and this tile's
   // header windows.
-  const Unit t0 = unit_of(P, gwave);
+  const Unit t0 = unit_of(P, tcur);
   glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
   vm_wait<0>();
-  glds<0>(desc_src(P, unit_of(P, gwave + W), lane), &L.desc[1][0]);
+  glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   {
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
 #ifndef OO_RX_ABL_NOHDR  // ablation builds (timing experiments only; results are wrong)
@@ -1702,20 +1738,28 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   }
 
   uint32_t b = 0, it_ = 0;
-  for (; it_ < K; b ^= 1u, ++it_) {
+  for (; tcur < P.ntiles; b ^= 1u, ++it_) {
     STAMP(0, __builtin_amdgcn_s_memrealtime());
-    const Unit tile = unit_of(P, gwave + it_ * W);
+    const Unit tile = unit_of(P, tcur);
     STAMP(6, tile.first);
     const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), tile, lane);
     const uint64_t zero = zero_line(P, tile, lane);
 
-    // ---- body jobs; the first R rounds land during the parse.
+    // ---- body jobs; the first R rounds land during the parse.  A tile with
+    // more than R + E rounds ("ext") also streams E rounds into the header
+    // rows during the demux: rounds 0..R-1 ring, R..R+E-1 header rows,
+    // R+E.. ring again; its next header windows are staged once the header
+    // rows are consumed.  T: the ring-loop rounds (a multiple of R; the
+    // padding rounds read zeros).
     uint32_t myslot;
     const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot);
-    uint32_t T = (J.T + R - 1) / R * R;  // whole ring turns; the padding rounds read zeros
+    uint32_t T0 = J.T;
 #ifdef OO_RX_ABL_NOBODY
-    T = 0;
+    T0 = 0;
 #endif
+    bool ext = E > 0 && T0 > (uint32_t)(R + E);
+    uint32_t T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
+    if (lane == 0) lds_write4(&L.T0, T0);
     IssueCursor ci;
     issue_slot(ci, J, 0, lane, zero);
     // This tile's header windows: older than the previous tile's NST stores
@@ -1729,20 +1773,33 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       if (it_ == 0) vm_wait<0>();
       else vm_wait<NSTK>();
     }
+
     STAMP(1, __builtin_amdgcn_s_memrealtime());
-    STAMP(7, T);
+    STAMP(7, T0);
+
+    // Rounds R..R+E-1 into the header rows, once their windows are read.
+    auto issue_extra = [&]() {
+      if (ext) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < E; ++u) issue_round(ci, J, zero, &L.hdr[u][0], lane);
+      }
+    };
 
     // ---- header work (one packet per lane).
     Parsed ps;
     TxHdr th;
     if constexpr (TX) {
       th = tx_header(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
+      issue_extra();
     } else {
 #ifdef OO_RX_ABL_NOPARSE
       ps = Parsed{};
       ps.r.reason = (uint8_t)(lds_read16(&L.hdr[0][lane]).x & 7u);
+      issue_extra();
 #else
       const Hdr h = parse_headers(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
+      issue_extra();
       STAMP(2, __builtin_amdgcn_s_memrealtime());
       ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
 #endif
@@ -1750,32 +1807,73 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     STAMP(3, __builtin_amdgcn_s_memrealtime());
 
     // ---- stage the next tile: descriptors of the tile after it into this
-    // tile's buffer, and its header windows.
-    glds<0>(desc_src(P, unit_of(P, gwave + (it_ + 2u) * W), lane), &L.desc[b][0]);
-    {
-      const Unit nt = unit_of(P, gwave + (it_ + 1u) * W);
+    // tile's buffer, its header windows (an ext tile: after its header-row
+    // rounds), and the claim of the tile after that.
+    T0 = sreg(lds_read4(&L.T0));
+    ext = E > 0 && T0 > (uint32_t)(R + E);
+    T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
+    // Tile i + 2: the claim issued at the previous tile (long landed).
+    if (it_ != 0)
+      tnext2 = P.dyn ? sreg(lds_read4(&L.dbase)) + (uint32_t)__builtin_amdgcn_readfirstlane((int)got)
+                     : tnext2 + W;
+    glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
+    auto stage_next = [&]() {
+      const Unit nt = unit_of(P, tnext);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
 #ifndef OO_RX_ABL_NOHDR
       stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
 #else
       (void)dn;
 #endif
-    }
+    };
+    if (!ext) stage_next();
+
+    claim_tile(P.claim + sreg(lds_read4(&L.gofs)), P.ngroups, lane, got);  // tile i + 3
 
     // The consume side's cursor is set up only now: its registers are free
     // during the header work, where the demux loads need them.
     ConsumeCursor cc;
     consume_start(cc, J, lane);
 
-    // ---- body stream (T is a multiple of R), two pieces per step.  Pieces
-    // newer than the awaited pair: the rest of the ring, plus the NHS
-    // staging operations in the first turn; none past T.
+    // ---- body stream, two pieces per step.  Each wait counts the
+    // operations issued after the awaited pair (the demux loads excepted:
+    // the demux waited for its last one, and with it for everything older).
+    if (ext) {
+      // Ring rounds 0..R-1, refilled with R+E..R+E+R-1: newer than the
+      // pair, the rest of the ring, the E header-row rounds, the descriptor
+      // line and the claim, and the refills so far -- R + E in all.
+#pragma unroll
+      for (int u = 0; u < R; u += 2) {
+        vm_wait<R + E>();
+        uint4 v0, v1;
+        lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
+        issue_round(ci, J, zero, &L.ring[u][0], lane);
+        issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
+      }
+      // Header-row rounds R..R+E-1: newer, the rest of them, the descriptor
+      // line and the claim, and the R refills.
+#pragma unroll
+      for (int u = 0; u < E; u += 2) {
+        vm_wait_n(R + E - u);
+        uint4 v0, v1;
+        lds_read16x2(&L.hdr[u][lane], &L.hdr[u + 1][lane], v0, v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
+      }
+      stage_next();
+    }
+    // The ring loop (T is a multiple of R).  Newer than the awaited pair: the
+    // rest of the ring, plus in the first turn the staging operations issued
+    // since the ring was filled (NHS, or HC after an ext prefix); none past T.
+    const int nhs = ext ? HC : NHS;
     for (uint32_t k0 = 0; k0 < T; k0 += R) {
       const bool first = k0 == 0, last = k0 + R == T;
 #pragma unroll
       for (int u = 0; u < R; u += 2) {
-        if (first && last) vm_wait_n(R - 2 - u + NHS);
-        else if (first) vm_wait_n(R - 2 + NHS);
+        if (first && last) vm_wait_n(R - 2 - u + nhs);
+        else if (first) vm_wait_n(R - 2 + nhs);
         else if (last) vm_wait_n(R - 2 - u);
         else vm_wait<R - 2>();
         uint4 v0, v1;
@@ -1802,14 +1900,31 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 #endif
     }
     STAMP(5, __builtin_amdgcn_s_memrealtime());
+    tcur = tnext;
+    tnext = tnext2;
   }
 
-  // Per-reason counts: one global atomic per reason seen by the wave.
+  // Per-reason counts: one global atomic per reason seen by the wave.  (The
+  // lane index is recomputed: kept live across the loop it would spill.)
+  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   if (!TX && P.counters != nullptr) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane < OO_RX_R_COUNT) {
-      const uint32_t c = lds_read4(&L.cnt[lane]);
-      if (c != 0) atomicAdd(&P.counters[lane], c);
+    if (ln < OO_RX_R_COUNT) {
+      const uint32_t c = lds_read4(&L.cnt[ln]);
+      if (c != 0) atomicAdd(&P.counters[ln], c);
+    }
+  }
+  }  // gwave < P.ntiles
+
+  // Every wave counts itself finished once its claims have been performed;
+  // the last of its group resets the group's counters for their next use.
+  vm_wait<0>();
+  if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
+    uint32_t* const ctr = P.claim + lds_read4(&L.gofs);  // {claims, finished}
+    const uint32_t done = atomicAdd(&ctr[1], 1u);
+    if (done == W / P.ngroups - 1u) {
+      atomicExch(&ctr[0], 0u);
+      atomicExch(&ctr[1], 0u);
     }
   }
 }

@@ -176,3 +176,27 @@ def test_full_size_config3_properties(cuda):
     buf, desc = pktgen.generate(3, 1 << 22)
     got = _check(g, o, buf, desc)
     assert (got["stage"][got["reason"] == 0] == 2).all()
+
+
+@pytest.mark.parametrize("env", [{"OO_RX_STATIC": "1"}, {"OO_RX_TAIL_TILE": "8", "OO_RX_TAIL_PER_WAVE": "3"},
+                                 {"OO_RX_TAIL_TILE": "64"}])
+def test_tile_partitions_and_claim_reuse(cuda, env, monkeypatch):
+    """Static and dynamic (claimed) tile schedules with several tail shapes
+    give the same records; 40 launches in a row reuse every claim-counter
+    set (16 per context) and must each see them reset (oo_rx_kernel.hip
+    tile_loop, oo_gpu_rx.cpp launch())."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    filters, socks = pktgen.world(5)
+    g = GpuRxStack(device=0)
+    o = OracleStack()
+    g.load_world(filters, socks)
+    o.load_world(filters, socks)
+    for n in (200003, 4099, 64, 1):
+        buf, desc = pktgen.generate(5, n, nthreads=NTHREADS)
+        want = o.handle_rx_batch(buf, desc, nthreads=NTHREADS)
+        for rep in range(10 if n > 1000 else 5):
+            got, ctr = run_dev(g, buf, desc)
+            assert got.tobytes() == want.tobytes(), (n, rep, diff_report(got, want, desc))
+            np.testing.assert_array_equal(ctr, counters_of(want))
+    g.close()

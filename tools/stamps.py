@@ -47,7 +47,7 @@ def main() -> None:
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
     out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     waves = grid * 4  # upper bound on waves per block
-    st = torch.zeros(waves * 64 * 8, dtype=torch.int64, device=dev)
+    st = torch.zeros(waves * 128 * 8, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
     g.sync(s)
     for _ in range(3):
@@ -58,7 +58,7 @@ def main() -> None:
     g.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
                           out.data_ptr(), 0, s)
     torch.cuda.synchronize(dev)
-    a = st.cpu().numpy().reshape(waves, 64, 8)
+    a = st.cpu().numpy().reshape(waves, 128, 8)
     used = a[:, :, 0] != 0
     t0 = a[:, :, 0][used].min()
     ns = 10.0  # s_memrealtime is 100 MHz
@@ -88,6 +88,28 @@ def main() -> None:
         "rounds_mean": float(ph[:, 7].mean()),
         "stream_ns_per_round": float((d(3, 4) / np.maximum(ph[:, 7], 1)).mean()),
     }
+    # Phase concurrency over time: the fraction of live waves streaming a
+    # body (stamps 3 -> 4) vs in the header phases (0 -> 3), in 1-us bins --
+    # synchronised header phases show as dips in the streaming fraction.
+    span = int(rows[:, 2].max() / 1e3) + 1
+    bins = np.arange(0, span + 1, 1.0)
+    strm = np.zeros(len(bins) - 1)
+    head = np.zeros(len(bins) - 1)
+    for w in range(waves):
+        for i in range(int(used[w].sum())):
+            t = (a[w, i, :6] - t0) * ns / 1e3
+            strm += np.histogram(np.linspace(t[3], t[4], 64), bins)[0] * ((t[4] - t[3]) / 64)
+            head += np.histogram(np.linspace(t[0], t[3], 16), bins)[0] * ((t[3] - t[0]) / 16)
+    live = strm + head
+    frac = np.where(live > 0, strm / np.maximum(live, 1e-9), 0)
+    res["stream_frac_by_us"] = {"min": float(frac[5:-40].min()) if span > 60 else None,
+                                "mean": float(frac[5:-40].mean()) if span > 60 else None,
+                                "first_12us": [round(float(x), 2) for x in frac[:12]],
+                                "p10_p90": [float(np.percentile(frac[5:-40], 10)),
+                                            float(np.percentile(frac[5:-40], 90))] if span > 60 else None}
+    res["per_tile_k_us"] = {str(k): [round(float(np.mean((a[used[:, k], k, j + 1] - a[used[:, k], k, j]) * ns / 1e3)), 2)
+                                     for j in range(5)]
+                            for k in range(min(int(used.sum(1).max()), 8)) if used[:, k].any()}
     # per-XCD view: blocks are dealt round-robin to the 8 XCDs
     wpb = max(1, waves // grid)
     ends = {}
