@@ -900,10 +900,11 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
   // The launch's claim counters (zero: every launch leaves them reset), one
-  // pair per wave group: the largest power of two <= CLAIM_GROUPS dividing W.
+  // pair per wave group: the largest power of two <= CLAIM_GROUPS and <= W
+  // (every group has a wave).
   P.claim = c->d_claim + 32u * CLAIM_GROUPS * (c->claim_seq++ % CLAIM_SLOTS);
   P.ngroups = 1;
-  while (P.ngroups < CLAIM_GROUPS && W % (2u * P.ngroups) == 0) P.ngroups *= 2;
+  while (P.ngroups < CLAIM_GROUPS && 2u * P.ngroups <= W) P.ngroups *= 2;
   P.dyn = c->dyn ? 1u : 0u;
   if (c->dyn) {
     // Dynamic: full 64-packet tiles, then about tail_per_wave tiles of

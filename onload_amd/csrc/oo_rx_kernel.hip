@@ -1594,8 +1594,8 @@ __device__ __forceinline__ void store_checks(const KParams& P, const DescView& d
 // a wave that runs fast takes more tiles and the waves finish together (the
 // host cuts the batch's end into small tiles, launch()).  Atomics on one
 // address serialise (~12 ns each), so the waves are split into P.ngroups
-// groups of W / ngroups waves (gwave mod ngroups, spread over all CUs), each
-// with its own counter over its own tiles (those = its group mod ngroups).
+// groups (gwave mod ngroups, spread over all CUs), each with its own counter
+// over its own tiles (those = its group mod ngroups).
 // The last wave of a group to finish resets the group's counters for the
 // launch that reuses them.
 
@@ -1713,6 +1713,8 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   const uint32_t W = gridDim.x * WAVES;
   // Tiles i, i + 1, i + 2 of this wave, and the claim of tile i + 3.
   uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
+  uint32_t claimed = 0;  // the last claim, once read (have)
+  bool have = false;
   // Group g's claims are g + 3 W, g + 3 W + ngroups, ... (its counter holds
   // the multiple of ngroups handed out); kept in LDS, out of the registers.
   if (lane == 0) {
@@ -1812,10 +1814,20 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     T0 = sreg(lds_read4(&L.T0));
     ext = E > 0 && T0 > (uint32_t)(R + E);
     T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
-    // Tile i + 2: the claim issued at the previous tile (long landed).
-    if (it_ != 0)
-      tnext2 = P.dyn ? sreg(lds_read4(&L.dbase)) + (uint32_t)__builtin_amdgcn_readfirstlane((int)got)
-                     : tnext2 + W;
+    // Tile i + 2: the claim issued at the previous tile, read at its end
+    // (have) or, after a tile without a body, here (the compiler waits for
+    // it: vmcnt(0), which a body-less tile has little in flight to pay for).
+    if (it_ != 0) {
+      uint32_t c;
+      if (have) {
+        c = claimed;
+      } else {
+        asm volatile("" ::: "memory");  // keeps the read (and its wait) on this path
+        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+      }
+      tnext2 = P.dyn ? sreg(lds_read4(&L.dbase)) + c : tnext2 + W;
+      have = false;
+    }
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
     auto stage_next = [&]() {
       const Unit nt = unit_of(P, tnext);
@@ -1886,6 +1898,12 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
         }
       }
     }
+    // The claim issued at this tile's staging has landed with the last body
+    // round (the ring loop ends on vmcnt(0)): reading it here costs nothing.
+    if (T != 0) {
+      claimed = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+      have = true;
+    }
     STAMP(4, __builtin_amdgcn_s_memrealtime());
 
     const uint32_t body = lane_get(cc.bs, myslot);
@@ -1921,8 +1939,11 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   vm_wait<0>();
   if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
     uint32_t* const ctr = P.claim + lds_read4(&L.gofs);  // {claims, finished}
+    // the group's waves: gwave = g mod ngroups (ngroups <= W, a power of two)
+    const uint32_t g = lds_read4(&L.gofs) / 32u;
+    const uint32_t members = W / P.ngroups + (g < (W & (P.ngroups - 1u)) ? 1u : 0u);
     const uint32_t done = atomicAdd(&ctr[1], 1u);
-    if (done == W / P.ngroups - 1u) {
+    if (done == members - 1u) {
       atomicExch(&ctr[0], 0u);
       atomicExch(&ctr[1], 0u);
     }
