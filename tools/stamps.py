@@ -47,7 +47,7 @@ def main() -> None:
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
     out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     waves = grid * 4  # upper bound on waves per block
-    st = torch.zeros(waves * 128 * 8, dtype=torch.int64, device=dev)
+    st = torch.zeros(waves * 128 * 16, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
     g.sync(s)
     for _ in range(3):
@@ -58,7 +58,7 @@ def main() -> None:
     g.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
                           out.data_ptr(), 0, s)
     torch.cuda.synchronize(dev)
-    a = st.cpu().numpy().reshape(waves, 128, 8)
+    a = st.cpu().numpy().reshape(waves, 128, 16)
     used = a[:, :, 0] != 0
     t0 = a[:, :, 0][used].min()
     ns = 10.0  # s_memrealtime is 100 MHz
@@ -88,6 +88,15 @@ def main() -> None:
         "rounds_mean": float(ph[:, 7].mean()),
         "stream_ns_per_round": float((d(3, 4) / np.maximum(ph[:, 7], 1)).mean()),
     }
+    # Inside the demux (slots 8-10, when the build stamps them): first-probe
+    # occupancy words landed, first records issued, stages walked.
+    dm = ph[:, 8] != 0
+    if dm.any():
+        q = ph[dm]
+        res["demux_us_mean"] = {"occ_words": float(((q[:, 8] - q[:, 2]) * ns).mean() / 1e3),
+                                "to_walks": float(((q[:, 9] - q[:, 8]) * ns).mean() / 1e3),
+                                "walks": float(((q[:, 10] - q[:, 9]) * ns).mean() / 1e3),
+                                "after_walks": float(((q[:, 3] - q[:, 10]) * ns).mean() / 1e3)}
     # Phase concurrency over time: the fraction of live waves streaming a
     # body (stamps 3 -> 4) vs in the header phases (0 -> 3), in 1-us bins --
     # synchronised header phases show as dips in the streaming fraction.
