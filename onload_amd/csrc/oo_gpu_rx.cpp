@@ -37,7 +37,7 @@ extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::Table
                                    uint32_t n, uint32_t gen, hipStream_t s);
 extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s);
 extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s);
-extern "C" int oo_table_launch_fp(const oo_rx::DevTables* T, hipStream_t s);
+extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s);
 
 namespace {
 
@@ -452,7 +452,7 @@ void mirror_from_image(oo_gpu_rx_ctx* c, const uint8_t* src) {
 // ---- Device lifetime.
 void free_dev(oo_gpu_rx_ctx* c) {
   DevTables& T = c->T;
-  for (void* p : {(void*)T.slot4, (void*)T.rc4, (void*)T.fp4,
+  for (void* p : {(void*)T.slot4, (void*)T.rc4, (void*)T.occ4, (void*)T.slot6, (void*)T.occ6,
                   (void*)T.socks, (void*)T.sockgen, (void*)c->d_zero, (void*)c->d_claim})
     if (p) (void)hipFree(p);
   for (OpStage& st : c->stage) {
@@ -653,9 +653,11 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   bool ok =
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
       hipEventCreateWithFlags(&c->tables_ev, hipEventDisableTiming) == hipSuccess &&
-      hipMalloc(&T.slot4, sizeof(Slot4) * n4 + sizeof(Slot6) * n6) == hipSuccess &&
+      hipMalloc(&T.slot4, sizeof(Slot4) * n4) == hipSuccess &&
       hipMalloc(&T.rc4, sizeof(int32_t) * n4) == hipSuccess &&
-      hipMalloc(&T.fp4, sizeof(uint64_t) * (n4 + n6)) == hipSuccess &&
+      hipMalloc(&T.occ4, sizeof(uint32_t) * ((n4 + 31) / 32)) == hipSuccess &&
+      hipMalloc(&T.slot6, sizeof(Slot6) * n6) == hipSuccess &&
+      hipMalloc(&T.occ6, sizeof(uint32_t) * ((n6 + 31) / 32)) == hipSuccess &&
       hipMalloc(&T.socks, sizeof(oo_gpu_rx_sock) * c->max_socks) == hipSuccess &&
       hipMalloc(&T.sockgen, sizeof(uint32_t) * c->max_socks) == hipSuccess &&
       hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + 64u * 32u) == hipSuccess &&
@@ -663,7 +665,6 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       hipMemsetAsync(c->d_claim, 0, 128u * CLAIM_SLOTS * CLAIM_GROUPS, c->stream) == hipSuccess &&
       hipHostMalloc(&c->h_image_hdr, sizeof(ImageHdr), hipHostMallocDefault) == hipSuccess &&
       hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
-      (T.slot6 = reinterpret_cast<Slot6*>(T.slot4 + n4), T.fp6 = T.fp4 + n4, true) &&
       oo_table_launch_init(&T, c->stream) == 0;
   for (OpStage& st : c->stage)
     ok = ok && hipHostMalloc(&st.h, sizeof(TableOp) * OPS_CHUNK, hipHostMallocDefault) == hipSuccess &&
@@ -853,7 +854,7 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, vo
           hipSuccess &&
       hipMemcpyAsync(c->T.socks, d + h.off_socks, sizeof(oo_gpu_rx_sock) * c->max_socks,
                      hipMemcpyDefault, s) == hipSuccess &&
-      oo_table_launch_fp(&c->T, s) == 0;
+      oo_table_launch_occ(&c->T, s) == 0;
   if (!ok) return -EIO;
   ++c->tables_gen;
   if (hipEventRecord(c->tables_ev, s) != hipSuccess) return -EIO;
@@ -887,9 +888,9 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.ip4_mask = c->ip4_mask;
   P.ip6_mask = c->ip6_mask;
   P.slot4 = c->T.slot4;
-  P.fp4 = c->T.fp4;
+  P.occ4 = c->T.occ4;
   P.slot6 = c->T.slot6;
-  P.fp6 = c->T.fp6;
+  P.occ6 = c->T.occ6;
   P.zero = c->d_zero;
   P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
   P.stamps = c->stamps;

@@ -43,29 +43,6 @@ OO_HD uint32_t hash2(uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp, uint32_
   return ((la ^ ra) ^ ((lp << 16) | rp) ^ proto) | 1u;
 }
 
-// Slot key fingerprints, kept beside the slot records (DevTables::fp4 /
-// fp6: one 8-B word per slot, {x = the entry's id/state word, y = key
-// fingerprint}).  y holds 16 bits of a mix of the entry's (laddr, lport,
-// protocol), 15 of its socket's (raddr, rport) and the socket's CONNECTED
-// bit (addresses as the XOR fold of their words, which only makes
-// fingerprints coarser).  A lookup key whose fingerprint differs from a
-// slot's cannot match it, so the demux loads a slot's record only when the
-// fingerprints agree, and confirms the match on the record (rec_match).
-OO_HD uint32_t fpmix(uint32_t h) {
-  h ^= h >> 16;
-  h *= 0x7feb352du;
-  h ^= h >> 15;
-  h *= 0x846ca68bu;
-  h ^= h >> 16;
-  return h;
-}
-OO_HD uint32_t fp_key(uint32_t lx, uint32_t lport, uint32_t proto, uint32_t rx, uint32_t rport,
-                      bool connected) {
-  const uint32_t a = fpmix(lx ^ (((lport << 16) | proto) * 0x9e3779b1u));
-  const uint32_t b = fpmix(rx ^ (rport * 0x85ebca6bu) ^ 0x2545f491u);
-  return (a & 0xffff0000u) | (b & 0x0000fffeu) | (connected ? 1u : 0u);
-}
-
 // Host mirror of the IPv6 filter table entry
 // ci_ip6_netif_filter_table_entry {id, route_count, laddr[16]}
 // (ip_shared_types.h:579-583).
@@ -86,10 +63,9 @@ static_assert(sizeof(oo_gpu_pkt_desc) == 16, "descriptor layout");
 // netif_table_ip6.c:110-189).  Here each slot is one record that already
 // carries the fields of the socket its id names, rebuilt by the host mirror
 // whenever the slot or that socket changes, so a visited slot is one 32-B
-// (IPv4) or 64-B (IPv6) load.  The slot fingerprints (fp_key above, 8 B per
-// slot: 512 KiB for 2^16 IPv4 slots) end most walks -- every walk ends at its
-// first EMPTY slot -- and pass over the slots that cannot match, without
-// touching the record array.
+// (IPv4) or 64-B (IPv6) load.  A bitmap of the slots that are not EMPTY
+// (1 bit per slot: 8 KiB for 2^16 IPv4 slots) ends most walks -- every walk
+// ends at its first EMPTY slot -- without touching the record array.
 struct Slot4 {
   uint32_t id_state;  // entry: id (30 bits) | state (2 bits), netif_table.c:34-42
   uint32_t laddr;     // entry
@@ -150,10 +126,9 @@ static_assert(sizeof(TableOp) == 64, "table op layout");
 struct DevTables {
   Slot4* slot4;
   int32_t* rc4;       // route counts of the IPv4 slots (the ext entries)
-  uint64_t* fp4;      // per IPv4 slot: id_state | fp_key << 32
-  Slot6* slot6;       // = slot4 + n4 (one allocation: the demux addresses both
-                      // tables as 32-bit offsets from slot4)
-  uint64_t* fp6;      // = fp4 + n4; per IPv6 slot: (uint32_t)id | fp_key << 32
+  uint32_t* occ4;     // bit i: IPv4 slot i is not EMPTY
+  Slot6* slot6;
+  uint32_t* occ6;
   oo_gpu_rx_sock* socks;
   uint32_t* sockgen;  // flush generation of each socket's last change
   uint32_t ip4_mask, ip6_mask, max_socks;
@@ -182,9 +157,9 @@ struct KParams {
   uint32_t ip4_mask;
   uint32_t ip6_mask;
   const Slot4* slot4;
-  const uint64_t* fp4;   // IPv4 slot fingerprints (DevTables::fp4)
-  const Slot6* slot6;    // = slot4 + ip4_mask + 1
-  const uint64_t* fp6;   // = fp4 + ip4_mask + 1: IPv6 slot fingerprints
+  const uint32_t* occ4;  // bit i set: IPv4 slot i is not EMPTY
+  const Slot6* slot6;
+  const uint32_t* occ6;  // bit i set: IPv6 slot i is not EMPTY
   const uint8_t* zero;   // ZERO_LINES x 16 B of zeros (lanes with nothing to read)
   uint8_t* sink;         // 64 x 32 B written by lanes without a packet (rx_kernel)
   uint64_t* stamps;      // diagnostic builds (OO_RX_STAMPS) only; may be null

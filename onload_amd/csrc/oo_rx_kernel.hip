@@ -184,7 +184,7 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
     if (P.stamps != nullptr && lane == 0 && it_ < 128)                               \
       P.stamps[((size_t)gwave * 128 + it_) * 16 + (ph)] = (val);                      \
   } while (0)
-// Inside the demux (phases 8..11): the tile loop points dstamp at its slots.
+// Inside the demux (phases 8..10): the tile loop points dstamp at its slots.
 __device__ uint64_t* dstamp_slot(uint64_t* p = nullptr, bool set = false) {
   static __shared__ uint64_t* slot[4];
   const uint32_t w = threadIdx.x >> 6;
@@ -232,6 +232,10 @@ struct Match {
   uint32_t n;
 };
 
+__device__ __forceinline__ bool occ_bit(const uint32_t* occ, uint32_t i) {
+  return ((occ[i >> 5] >> (i & 31u)) & 1u) != 0;
+}
+
 // ci_sock_intf_check (netif_table.h:30-36) on the socket fields of a slot.
 __device__ __forceinline__ bool bind2dev_ok(const KParams& P, uint32_t sflags, uint64_t hwports,
                                             int b2d_vlan, int intf_i, int vlan) {
@@ -253,7 +257,7 @@ struct Rec {
 // addresses are picked from the (scalar) kernel arguments at each use: held
 // per lane they would be loop-invariant VGPRs the kernel cannot afford.
 struct Probe {
-  uint32_t fpo, slo;  // this lane's table: byte offsets from P.fp4 / P.slot4
+  uint64_t occ, slots;  // this lane's table (per tile: not loop-invariant)
   uint32_t mask;
   bool is6;
 };
@@ -291,66 +295,47 @@ __device__ __forceinline__ Probe probe_of(const KParams& P, bool is6) {
   Probe t;
   t.is6 = is6;
   t.mask = is6 ? sreg(P.ip6_mask) : sreg(P.ip4_mask);
-  // The IPv6 tables follow the IPv4 ones in the same allocations
-  // (oo_rx_device.h DevTables), so both are 32-bit offsets from one base.
-  t.fpo = is6 ? (sreg(P.ip4_mask) + 1u) * 8u : 0u;
-  t.slo = is6 ? (sreg(P.ip4_mask) + 1u) * (uint32_t)sizeof(Slot4) : 0u;
+  t.occ = sel64(is6, sreg64(P.occ6), sreg64(P.occ4));
+  t.slots = sel64(is6, sreg64(P.slot6), sreg64(P.slot4));
   return t;
 }
 
-// The fingerprint words (oo_rx_device.h fp_key) of six slots (every stage's
-// first slot and its successor) in one batch: six loads, one wait.  Written
-// as one asm block because the register-bound scheduler otherwise consumes
-// each load before issuing the next (six memory latencies instead of one).
-// The wait is vmcnt(0): loads complete in issue order and these are the
-// newest, so it waits for nothing they would not.
-__device__ __forceinline__ void fp_words6(const KParams& P, const Probe& t, const uint32_t i[6],
-                                          uint64_t f[6]) {
-  const uint64_t base = sreg64(P.fp4);
-  uint32_t a[6];
+// The occupancy words of six slots (every stage's first slot and its
+// successor) in one batch: six loads, one wait.  Written as one asm block
+// because the register-bound scheduler otherwise consumes each load before
+// issuing the next (six memory latencies instead of one).  The wait is
+// vmcnt(0): loads complete in issue order and these are the newest, so it
+// waits for nothing they would not.
+__device__ __forceinline__ void occ_words6(const Probe& t, const uint32_t i[6], uint32_t w[6]) {
+  uint64_t a[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) a[k] = t.fpo + 8u * i[k];
-#ifdef OO_RX_DEBUG_TABLES
-  typedef const __attribute__((address_space(1))) uint64_t* g_cu64p;
-  const uint32_t lf = (sreg(P.ip4_mask) + sreg(P.ip6_mask) + 2u) * 8u;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    if (a[k] + 8u > lf) {
-      printf("oob fp6: is6 %d k %d i %u a %u mask %u\n", (int)t.is6, k, i[k], a[k], t.mask);
-      a[k] = 0;
-    }
-    f[k] = *reinterpret_cast<g_cu64p>(base + a[k]);
-  }
-  return;
-#endif
+  for (int k = 0; k < 6; ++k) a[k] = t.occ + 4u * (i[k] >> 5);
   asm volatile(
-      "s_nop 4\n\tglobal_load_dwordx2 %0, %6, %12\n\tglobal_load_dwordx2 %1, %7, %12\n\t"
-      "global_load_dwordx2 %2, %8, %12\n\tglobal_load_dwordx2 %3, %9, %12\n\t"
-      "global_load_dwordx2 %4, %10, %12\n\tglobal_load_dwordx2 %5, %11, %12\n\t"
+      "global_load_dword %0, %6, off\n\tglobal_load_dword %1, %7, off\n\t"
+      "global_load_dword %2, %8, off\n\tglobal_load_dword %3, %9, off\n\t"
+      "global_load_dword %4, %10, off\n\tglobal_load_dword %5, %11, off\n\t"
       "s_waitcnt vmcnt(0)"
-      : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5])
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "s"(base)
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5])
       : "memory");
 }
 
-// What a slot's fingerprint word says about it for one lookup key (kfp, the
-// key's fp_key; full: the stage compares raddr/rport -- otherwise, IPv6
-// wildcard stages, the socket must not be connected): EMPTY ends the walk;
-// a candidate's record must be loaded and compared (rec_match); any other
-// slot (tombstone, a different key, or an IPv4 first probe that is not
-// PREFERRED) is passed over.
-struct SlotFp {
-  bool empty, cand;
-};
-__device__ __forceinline__ SlotFp fp_test(uint64_t f, bool is6, bool first, uint32_t kfp,
-                                          bool full) {
-  const uint32_t x = (uint32_t)f, y = (uint32_t)(f >> 32);
-  const uint32_t d = kfp ^ y;
-  const bool occ = is6 ? (int32_t)x >= 0
-                       : first ? (x & ST_MASK) == ST_PREFERRED : occupied(x);
-  SlotFp r;
-  r.empty = is6 ? (int32_t)x == ID6_EMPTY : (x & ST_MASK) == ST_EMPTY;
-  r.cand = occ && (d >> 16) == 0 && (full ? (d & 0xfffeu) == 0 : (y & 1u) == 0);
+__device__ __forceinline__ bool probe_occ(const KParams& P, const Probe& t, uint32_t i) {
+  (void)P;
+  return ((gload4(t.occ + 4u * (i >> 5)) >> (i & 31u)) & 1u) != 0;
+}
+
+__device__ __forceinline__ Rec load_rec(const KParams& P, const Probe& t, uint32_t i, bool any6) {
+  (void)P;
+  const uint64_t a = t.slots + ((uint64_t)i << (t.is6 ? 6 : 5));
+  Rec r;
+  r.d0 = gload16(a);
+  r.d1 = gload16(a + 16u);
+  r.d2 = r.d3 = make_uint4(0, 0, 0, 0);
+  if (any6 && t.is6) {
+    r.d2 = gload16(a + 32u);
+    r.d3 = gload16(a + 48u);
+  }
   return r;
 }
 
@@ -393,6 +378,45 @@ __device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool f
     hw = (uint64_t)r.d3.z | ((uint64_t)r.d3.w << 32);
   }
   return ok && bind2dev_ok(P, sflags, hw, b2d, intf_i, vlan);
+}
+
+// ci_netif_filter_for_each_match (netif_table.c:234-319) /
+// ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189) over the
+// slot records, every match counted.  The caller has loaded the not-EMPTY
+// bits of the first slot (occ) and of the next one on the probe sequence
+// (occ_next), and -- when have -- the first slot's record: the common walk
+// (an EMPTY first slot, or one occupied slot followed by an EMPTY one) needs
+// no more loads.  Tombstones continue the walk; an EMPTY slot or a full
+// cycle ends it.
+template <bool IS6>
+__device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_t la[4],
+                      uint32_t lp, const uint32_t ra[4], bool ra_null, uint32_t rp, uint32_t proto,
+                      int intf_i, int vlan, uint32_t h1, uint32_t h2, bool occ, Rec rec, bool have,
+                      bool occ_next) {
+  Match m = {-1, 0};
+  const uint32_t first = h1;
+  if (occ && !have) rec = load_rec(P, t, h1, any6);  // the first slot's record was not preloaded
+  for (uint32_t guard = 0; guard <= t.mask; ++guard) {
+    if (!occ) break;  // an EMPTY slot ends the walk
+    int32_t id;
+    if (rec_match<IS6>(P, rec, guard == 0, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id)) {
+      if (m.n == 0) m.first = id;
+      ++m.n;
+    }
+    h1 = (h1 + h2) & t.mask;
+    if (h1 == first) break;
+    if (guard == 0) {
+      occ = occ_next;
+      if (occ) rec = load_rec(P, t, h1, any6);
+    } else {
+      // Deeper in a chain: the record is loaded beside its occupancy bit
+      // (one load latency per step, not two; an EMPTY slot's record is
+      // simply not used).
+      rec = load_rec(P, t, h1, any6);
+      occ = probe_occ(P, t, h1);
+    }
+  }
+  return m;
 }
 
 // ---------------------------------------------------------------------------
@@ -834,226 +858,41 @@ __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, u
   return h;
 }
 
-// The lookup stages of one lane -- ci_netif_filter_for_each_match
-// (netif_table.c:234-319) / ci_netif_filter_for_each_match_ip6
-// (netif_table_ip6.c:110-189) for the keys of ci_udp_handle_rx (udp_rx.c:
-// 271-306: full 4-tuple, then (laddr, lport)) or ci_tcp_handle_rx
-// (tcp_rx.c:4786-4835: then (*, lport)), every match of a stage counted; the
+// The 2 (UDP) or 3 (TCP) lookup stages of one lane in reference order; the
 // first stage with a match decides (*stage = 1..3).
-//
-// The stages are walked together, not one after another: each step of the
-// loop issues, for every lane, the fingerprint word of the next slot of each
-// stage still walking and the record of one candidate slot, then waits once.
-// A wave's demux thus pays as many dependent loads as its longest walk, not
-// their sum over stages and address families -- each such load waits behind
-// the body stream in flight, so their number is what the demux costs.  Per
-// stage: candidates at the first slot (c0) and the next (c1) come from the
-// fingerprint words loaded with the key (fp_words6); deeper slots are walked
-// one per step (act, at pos) and hold one candidate at a time (cd, at pd),
-// the walk pausing until that record is checked.  Records are checked in walk
-// order (c0, c1, then the deep ones), so a stage's first match is the
-// reference's.  A stage with a match ends the stages after it.
-// The loads of one walk step -- a record (slot i; IPv4 lanes of an ANY6
-// wave read their 32-B record twice) and three fingerprint words -- issued
-// together and waited for once (as fp_words6, one asm block: the compiler
-// otherwise waits for the record before issuing the words).  The table bases
-// are SGPR operands, often reloaded from a spill lane (v_readlane, a VALU
-// write of an SGPR) just before the block; a VMEM read of an SGPR needs 5
-// wait states after such a write, which the compiler does not insert for
-// inline asm -- hence the s_nop 4 that opens each of these blocks.
-template <bool ANY6>
-__device__ __forceinline__ void step_loads(const KParams& P, const Probe& t, uint32_t i,
-                                           uint32_t p0, uint32_t p1, uint32_t p2, Rec& r,
-                                           uint64_t fd[3]) {
-  const uint64_t sb = sreg64(P.slot4), fb = sreg64(P.fp4);
-  const uint32_t a = t.slo + (i << (t.is6 ? 6 : 5));
-  const uint32_t f0 = t.fpo + 8u * p0, f1 = t.fpo + 8u * p1, f2 = t.fpo + 8u * p2;
-  u32x4 d0, d1, d2, d3;
-#ifdef OO_RX_DEBUG_TABLES
-  {
-    const uint32_t ls = (sreg(P.ip4_mask) + 1u) * 32u + (sreg(P.ip6_mask) + 1u) * 64u;
-    const uint32_t lf = (sreg(P.ip4_mask) + sreg(P.ip6_mask) + 2u) * 8u;
-    const uint32_t b = ANY6 && t.is6 ? a + 32u : a;
-    const bool bad = b + 32u > ls || f0 + 8u > lf || f1 + 8u > lf || f2 + 8u > lf;
-    if (bad)
-      printf("oob step: is6 %d i %u p %u %u %u a %u f %u %u %u mask %u\n", (int)t.is6, i, p0, p1,
-             p2, a, f0, f1, f2, t.mask);
-    const uint64_t A = sb + (bad ? 0u : a), B = sb + (bad ? 0u : b);
-    d0 = *reinterpret_cast<g_cu32x4p>(A);
-    d1 = *reinterpret_cast<g_cu32x4p>(A + 16u);
-    d2 = ANY6 ? *reinterpret_cast<g_cu32x4p>(B) : u32x4{0, 0, 0, 0};
-    d3 = ANY6 ? *reinterpret_cast<g_cu32x4p>(B + 16u) : u32x4{0, 0, 0, 0};
-    typedef const __attribute__((address_space(1))) uint64_t* g_cu64p;
-    fd[0] = *reinterpret_cast<g_cu64p>(fb + (bad ? 0u : f0));
-    fd[1] = *reinterpret_cast<g_cu64p>(fb + (bad ? 0u : f1));
-    fd[2] = *reinterpret_cast<g_cu64p>(fb + (bad ? 0u : f2));
+template <bool IS6>
+__device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t, bool any6,
+                                               const Hdr& h, uint32_t dport, uint32_t sport,
+                                               uint32_t proto, int intf_i, int vlan, bool tcp,
+                                               uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
+                                               bool o0, bool o1, bool o2, bool q0, bool q1,
+                                               bool q2, Rec rec, int fs, int& stage) {
+  const uint32_t zero[4] = {0, 0, 0, 0};
+  const uint32_t dx = IS6 ? (h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3]) : h.da[0];
+  const uint32_t sx = IS6 ? (h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3]) : h.sa[0];
+  Match m = walk<IS6>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
+                      hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0);
+  stage = 1;
+  if (m.n == 0) {
+    m = walk<IS6>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
+                  hash2(dx, dport, 0u, 0u, proto), o1, rec, fs == 1, q1);
+    stage = 2;
   }
-#else
-  if (ANY6) {
-    const uint32_t b = t.is6 ? a + 32u : a;
-    asm volatile(
-        "s_nop 4\n\tglobal_load_dwordx4 %0, %7, %12\n\tglobal_load_dwordx4 %1, %7, %12 offset:16\n\t"
-        "global_load_dwordx4 %2, %8, %12\n\tglobal_load_dwordx4 %3, %8, %12 offset:16\n\t"
-        "global_load_dwordx2 %4, %9, %13\n\tglobal_load_dwordx2 %5, %10, %13\n\t"
-        "global_load_dwordx2 %6, %11, %13\n\ts_waitcnt vmcnt(0)"
-        : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(fd[0]), "=&v"(fd[1]), "=&v"(fd[2])
-        : "v"(a), "v"(b), "v"(f0), "v"(f1), "v"(f2), "s"(sb), "s"(fb)
-        : "memory");
-  } else {
-    asm volatile(
-        "s_nop 4\n\tglobal_load_dwordx4 %0, %5, %9\n\tglobal_load_dwordx4 %1, %5, %9 offset:16\n\t"
-        "global_load_dwordx2 %2, %6, %10\n\tglobal_load_dwordx2 %3, %7, %10\n\t"
-        "global_load_dwordx2 %4, %8, %10\n\ts_waitcnt vmcnt(0)"
-        : "=&v"(d0), "=&v"(d1), "=&v"(fd[0]), "=&v"(fd[1]), "=&v"(fd[2])
-        : "v"(a), "v"(f0), "v"(f1), "v"(f2), "s"(sb), "s"(fb)
-        : "memory");
-    d2 = d3 = u32x4{0, 0, 0, 0};
+  if (m.n == 0 && tcp) {
+    m = walk<IS6>(P, t, any6, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2,
+                  hash2(0u, dport, 0u, 0u, proto), o2, rec, fs == 2, q2);
+    stage = 3;
   }
-#endif
-  r.d0 = make_uint4(d0.x, d0.y, d0.z, d0.w);
-  r.d1 = make_uint4(d1.x, d1.y, d1.z, d1.w);
-  r.d2 = make_uint4(d2.x, d2.y, d2.z, d2.w);
-  r.d3 = make_uint4(d3.x, d3.y, d3.z, d3.w);
-}
-
-struct StageWalk {
-  uint32_t h1, h2, kfp;  // first slot, step, key fingerprint
-  uint32_t pos, pd;      // next deep slot (its word loaded by the step); deep candidate
-  bool c0, c1, act, cd;
-  Match m;
-};
-
-template <bool ANY6>
-__device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t, const Hdr& h,
-                                               uint32_t dx, uint32_t sx, uint32_t dport,
-                                               uint32_t sport, uint32_t proto, int intf_i,
-                                               int vlan, bool tcp, bool look, int& stage) {
-  const bool six = ANY6 && t.is6;
-  StageWalk w[3];
-  w[0].h1 = hash3(dx, dport, sx, sport, proto) & t.mask;
-  w[1].h1 = hash3(dx, dport, 0u, 0u, proto) & t.mask;
-  w[2].h1 = hash3(0u, dport, 0u, 0u, proto) & t.mask;
-  w[0].h2 = hash2(dx, dport, sx, sport, proto);
-  w[1].h2 = hash2(dx, dport, 0u, 0u, proto);
-  w[2].h2 = hash2(0u, dport, 0u, 0u, proto);
-  // The IPv6 wildcard stages test CONNECTED instead of raddr/rport.
-  w[0].kfp = fp_key(dx, dport, proto, sx, sport, false);
-  w[1].kfp = fp_key(dx, dport, proto, 0u, 0u, false);
-  w[2].kfp = fp_key(0u, dport, proto, 0u, 0u, false);
-  uint32_t n1[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    n1[k] = (w[k].h1 + w[k].h2) & t.mask;
-    w[k].c0 = w[k].c1 = w[k].act = w[k].cd = false;
-    w[k].pos = w[k].pd = 0;
-    w[k].m = Match{-1, 0};
-  }
-  if (look) {
-    // Both first slots of all three stages in one batch (a UDP lane's
-    // stage-3 words are unused).
-    const uint32_t idx[6] = {w[0].h1, w[1].h1, w[2].h1, n1[0], n1[1], n1[2]};
-    uint64_t f[6];
-    fp_words6(P, t, idx, f);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const bool full = k == 0 || !six;
-      const SlotFp a = fp_test(f[k], six, true, w[k].kfp, full);
-      const SlotFp b = fp_test(f[3 + k], six, false, w[k].kfp, full);
-      const bool live = k < 2 || tcp;
-      const bool go1 = live && !a.empty && n1[k] != w[k].h1;  // a one-slot table ends here
-      w[k].c0 = live && !a.empty && a.cand;
-      w[k].c1 = go1 && !b.empty && b.cand;
-      w[k].pos = (n1[k] + w[k].h2) & t.mask;
-      w[k].act = go1 && !b.empty && w[k].pos != w[k].h1;
-    }
-  }
-  DSTAMP(8);
-  for (uint32_t guard = 0; guard <= 3u * t.mask + 8u; ++guard) {
-    // The record to check: the first pending candidate in stage and walk order.
-    int rs = -1;
-    uint32_t rslot = 0;
-    bool rfirst = false;
-#pragma unroll
-    for (int k = 2; k >= 0; --k) {
-      if (w[k].cd) { rs = k; rslot = w[k].pd; rfirst = false; }
-      if (w[k].c1) { rs = k; rslot = n1[k]; rfirst = false; }
-      if (w[k].c0) { rs = k; rslot = w[k].h1; rfirst = true; }
-    }
-    bool ld[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ld[k] = w[k].act && !w[k].cd;
-    if (__ballot(rs >= 0 || ld[0] || ld[1] || ld[2]) == 0) break;
-    // One batch for every lane (a lane with nothing to load reads slot 0).
-    Rec rec;
-    uint64_t fd[3];
-    step_loads<ANY6>(P, t, rs >= 0 ? rslot : 0u, ld[0] ? w[0].pos : 0u, ld[1] ? w[1].pos : 0u,
-                     ld[2] ? w[2].pos : 0u, rec, fd);
-    if (rs >= 0) {
-      // The stage's key: (daddr, dport, saddr, sport), (daddr, dport, -, -),
-      // (-, dport, -, -).
-      uint32_t la[4], ra[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        la[i] = rs == 2 ? 0u : h.da[i];
-        ra[i] = rs == 0 ? h.sa[i] : 0u;
-      }
-      const uint32_t rp = rs == 0 ? sport : 0u;
-      int32_t id;
-      const bool ok =
-          (ANY6 && six)
-              ? rec_match<true>(P, rec, false, la, dport, ra, rs != 0, rp, proto, intf_i, vlan, id)
-              : rec_match<false>(P, rec, rfirst, la, dport, ra, rs != 0, rp, proto, intf_i, vlan,
-                                 id);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        if (rs != k) continue;
-        if (ok) {
-          if (w[k].m.n == 0) w[k].m.first = id;
-          ++w[k].m.n;
-        }
-        if (w[k].c0) w[k].c0 = false;
-        else if (w[k].c1) w[k].c1 = false;
-        else w[k].cd = false;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      if (!ld[k]) continue;
-      const SlotFp c = fp_test(fd[k], six, false, w[k].kfp, k == 0 || !six);
-      if (c.empty) {
-        w[k].act = false;
-      } else {
-        if (c.cand) {
-          w[k].cd = true;
-          w[k].pd = w[k].pos;
-        }
-        w[k].pos = (w[k].pos + w[k].h2) & t.mask;
-        if (w[k].pos == w[k].h1) w[k].act = false;  // a full cycle
-      }
-    }
-    // A stage with a match decides: the stages after it are not needed.
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (w[k].m.n == 0) continue;
-#pragma unroll
-      for (int j = k + 1; j < 3; ++j) w[j].c0 = w[j].c1 = w[j].act = w[j].cd = false;
-    }
-  }
-  // Field by field: a select of whole structs becomes a scratch access.
-  const bool s0 = w[0].m.n != 0, s1 = w[1].m.n != 0;
-  stage = s0 ? 1 : s1 ? 2 : 3;
-  Match m;
-  m.n = s0 ? w[0].m.n : s1 ? w[1].m.n : w[2].m.n;
-  m.first = s0 ? w[0].m.first : s1 ? w[1].m.first : w[2].m.first;
   return m;
 }
 
 // The record of one packet from its headers: the lookup stages of
 // ci_udp_handle_rx (udp_rx.c:271-306: full 4-tuple, then (laddr, lport)) or
 // ci_tcp_handle_rx (tcp_rx.c:4786-4835: then (*, lport)); the first stage
-// with a match decides.  IPv4 and IPv6 lanes share one instruction stream
-// (lookup_stages), so a wave pays the same dependent loads however its
-// packets mix address families and protocols.
+// with a match decides.  IPv4 and IPv6 lanes share one instruction stream:
+// every stage's first-slot and next-slot occupancy bits are loaded together,
+// then the first slots' records, so a wave pays two dependent loads however
+// its packets mix address families and protocols.
 template <bool ANY6>
 __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h, int intf_i,
                                                  uint64_t abase, int span, int shift) {
@@ -1089,14 +928,42 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     look = reason == PENDING;
   }
   if (__ballot(look) != 0) {
+    constexpr bool any6 = ANY6;
     const uint32_t sport = h.sport, dport = h.dport;
     const uint32_t dx = r.daddr_be, sx = r.saddr_be;  // hash addresses
     const Probe t = probe_of(P, ANY6 && is6);
     const bool tcp = proto == 6u;
-    Match m;
-    int stage;
-    m = lookup_stages<ANY6>(P, t, h, dx, sx, dport, sport, proto, intf_i, vlan, tcp, look, stage);
+    const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & t.mask;
+    const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & t.mask;
+    const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & t.mask;
+    const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
+    const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
+    const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
+    // All six bits in one batch (a UDP lane's stage-3 bits are unused).
+    bool o0 = false, o1 = false, o2 = false, q0 = false, q1 = false, q2 = false;
     if (look) {
+      const uint32_t idx[6] = {h1_0, h1_1, h1_2, (h1_0 + h2_0) & t.mask, (h1_1 + h2_1) & t.mask,
+                               (h1_2 + h2_2) & t.mask};
+      uint32_t w[6];
+      occ_words6(t, idx, w);
+      DSTAMP(8);
+      auto bit = [&](int k) { return ((w[k] >> (idx[k] & 31u)) & 1u) != 0; };
+      o0 = bit(0);
+      o1 = bit(1);
+      o2 = bit(2) && tcp;
+      q0 = bit(3);
+      q1 = bit(4);
+      q2 = bit(5) && tcp;
+    }
+    // One record per lane up front: the first slot of the first stage whose
+    // first slot is occupied (a stage with an EMPTY first slot ends at once,
+    // and that record usually decides); a later stage loads its own only
+    // when this one did not match.
+    const int fs = o0 ? 0 : o1 ? 1 : o2 ? 2 : 3;
+    Rec rec = {};
+    if (look && fs < 3) rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
+    if (look) {
+      DSTAMP(9);
       r.hash3 = hash3(dx, dport, sx, sport, proto);
       if (proto == 17u) {
         // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
@@ -1105,6 +972,15 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
         const uint32_t dd = is6 ? h.sa[2] : h.da[0];
         if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
       }
+      // The walks compare per address family (divergent only in waves that
+      // hold both): the loads above were shared.
+      Match m;
+      int stage;
+      if (ANY6 && is6) m = lookup_stages<true>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp,
+                                               h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs,
+                                               stage);
+      else m = lookup_stages<false>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0,
+                                    h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
       DSTAMP(10);
       reason = OO_RX_R_NO_MATCH;
       if (m.n) {

@@ -34,30 +34,9 @@
 
 namespace oo_rx {
 
-// A slot's fingerprint word (oo_rx_device.h fp_key) from its record; every
-// record write goes through put4 / put6 so the two never disagree.
-__device__ __forceinline__ uint64_t fp_of4(const Slot4& r) {
-  const uint32_t y = occupied(r.id_state)
-                         ? fp_key(r.laddr, r.lport, r.proto, r.raddr, r.rport,
-                                  (r.sflags & OO_GPU_RX_SOCK_CONNECTED) != 0)
-                         : 0u;
-  return (uint64_t)r.id_state | ((uint64_t)y << 32);
-}
-__device__ __forceinline__ uint64_t fp_of6(const Slot6& r) {
-  const uint32_t lx = r.laddr[0] ^ r.laddr[1] ^ r.laddr[2] ^ r.laddr[3];
-  const uint32_t rx = r.raddr[0] ^ r.raddr[1] ^ r.raddr[2] ^ r.raddr[3];
-  const uint32_t y = r.id >= 0 ? fp_key(lx, r.lport, r.proto, rx, r.rport,
-                                        (r.sflags & OO_GPU_RX_SOCK_CONNECTED) != 0)
-                               : 0u;
-  return (uint64_t)(uint32_t)r.id | ((uint64_t)y << 32);
-}
-__device__ __forceinline__ void put4(const DevTables& T, uint32_t i, const Slot4& r) {
-  T.slot4[i] = r;
-  T.fp4[i] = fp_of4(r);
-}
-__device__ __forceinline__ void put6(const DevTables& T, uint32_t i, const Slot6& r) {
-  T.slot6[i] = r;
-  T.fp6[i] = fp_of6(r);
+__device__ __forceinline__ void occ_set(uint32_t* occ, uint32_t i, bool on) {
+  const uint32_t b = 1u << (i & 31u);
+  occ[i >> 5] = on ? (occ[i >> 5] | b) : (occ[i >> 5] & ~b);
 }
 
 // The socket fields of slot records (what netif_table.c:192-231 reads through
@@ -118,7 +97,8 @@ __device__ void ip4_insert(const DevTables& T, const TableOp& op) {
   r.laddr = la;
   r.lport = op.lport;
   slot4_sock(r, T.socks[op.sock]);
-  put4(T, h1, r);
+  T.slot4[h1] = r;
+  occ_set(T.occ4, h1, true);
 }
 
 // ci_ip4_netif_filter_remove + __ci_ip4_netif_filter_remove.
@@ -144,7 +124,8 @@ __device__ void ip4_remove(const DevTables& T, const TableOp& op) {
     Slot4 r = T.slot4[k];
     r.id_state = (r.id_state & ID_MASK) | ST_EMPTY;
     slot4_nosock(r);
-    put4(T, k, r);
+    T.slot4[k] = r;
+    occ_set(T.occ4, k, false);
   };
   i = h1;
   for (int k = 0; k < hops; ++k) {
@@ -154,9 +135,7 @@ __device__ void ip4_remove(const DevTables& T, const TableOp& op) {
   if (T.rc4[i] == 0) {
     to_empty(i);
   } else {
-    Slot4 r = T.slot4[i];
-    r.id_state = (r.id_state & ID_MASK) | ST_TOMBSTONE;
-    put4(T, i, r);
+    T.slot4[i].id_state = (T.slot4[i].id_state & ID_MASK) | ST_TOMBSTONE;
   }
 }
 
@@ -184,7 +163,8 @@ __device__ void ip6_insert(const DevTables& T, const TableOp& op) {
   r.id = op.sock;
   for (int k = 0; k < 4; ++k) r.laddr[k] = op.u.t.la[k];
   slot6_sock(r, T.socks[op.sock]);
-  put6(T, h1, r);
+  T.slot6[h1] = r;
+  occ_set(T.occ6, h1, true);
 }
 
 // ci_ip6_netif_filter_remove: a tombstone loses its id (-1).
@@ -209,7 +189,8 @@ __device__ void ip6_remove(const DevTables& T, const TableOp& op) {
     Slot6 r = T.slot6[k];
     r.id = nid;
     slot6_nosock(r);
-    put6(T, k, r);
+    T.slot6[k] = r;
+    occ_set(T.occ6, k, nid != ID6_EMPTY);
   };
   i = h1;
   for (int k = 0; k < hops; ++k) {
@@ -251,7 +232,7 @@ __global__ __launch_bounds__(256) void table_refresh(DevTables T, uint32_t gen) 
       if ((st & ST_MASK) != ST_EMPTY && id < T.max_socks && T.sockgen[id] == gen) {
         Slot4 r = T.slot4[i];
         slot4_sock(r, T.socks[id]);
-        put4(T, i, r);
+        T.slot4[i] = r;
       }
     } else {
       const uint32_t j = i - n4;
@@ -259,14 +240,14 @@ __global__ __launch_bounds__(256) void table_refresh(DevTables T, uint32_t gen) 
       if (id >= 0 && (uint32_t)id < T.max_socks && T.sockgen[id] == gen) {
         Slot6 r = T.slot6[j];
         slot6_sock(r, T.socks[id]);
-        put6(T, j, r);
+        T.slot6[j] = r;
       }
     }
   }
 }
 
 // Fresh tables: every slot EMPTY (netif_table.c:592-611: IPv4 state EMPTY,
-// netif_table_ip6.c:349-365: id -2), no sockets.
+// netif_table_ip6.c:349-365: id -2), no sockets, no occupancy.
 __global__ __launch_bounds__(256) void table_init(DevTables T) {
   const uint32_t n4 = T.ip4_mask + 1u, n6 = T.ip6_mask + 1u;
   const uint32_t total = n4 + n6 + T.max_socks;
@@ -275,13 +256,15 @@ __global__ __launch_bounds__(256) void table_init(DevTables T) {
     if (i < n4) {
       Slot4 r = {};
       r.id_state = ST_EMPTY;
-      put4(T, i, r);
+      T.slot4[i] = r;
       T.rc4[i] = 0;
+      if ((i & 31u) == 0) T.occ4[i >> 5] = 0;
     } else if (i < n4 + n6) {
       const uint32_t j = i - n4;
       Slot6 r = {};
       r.id = ID6_EMPTY;
-      put6(T, j, r);
+      T.slot6[j] = r;
+      if ((j & 31u) == 0) T.occ6[j >> 5] = 0;
     } else {
       const uint32_t k = i - n4 - n6;
       T.socks[k] = oo_gpu_rx_sock{};
@@ -290,13 +273,22 @@ __global__ __launch_bounds__(256) void table_init(DevTables T) {
   }
 }
 
-// Fingerprints from the slot records (after an image import).
-__global__ __launch_bounds__(256) void table_fp(DevTables T) {
-  const uint32_t n4 = T.ip4_mask + 1u, n6 = T.ip6_mask + 1u;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4 + n6;
-       i += gridDim.x * blockDim.x) {
-    if (i < n4) T.fp4[i] = fp_of4(T.slot4[i]);
-    else T.fp6[i - n4] = fp_of6(T.slot6[i - n4]);
+// Occupancy bits from the slot records (after an image import).
+__global__ __launch_bounds__(256) void table_occ(DevTables T) {
+  const uint32_t w4 = (T.ip4_mask + 1u + 31u) >> 5, w6 = (T.ip6_mask + 1u + 31u) >> 5;
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < w4 + w6;
+       w += gridDim.x * blockDim.x) {
+    uint32_t bits = 0;
+    if (w < w4) {
+      for (uint32_t b = 0; b < 32u && w * 32u + b <= T.ip4_mask; ++b)
+        if ((T.slot4[w * 32u + b].id_state & ST_MASK) != ST_EMPTY) bits |= 1u << b;
+      T.occ4[w] = bits;
+    } else {
+      const uint32_t v = w - w4;
+      for (uint32_t b = 0; b < 32u && v * 32u + b <= T.ip6_mask; ++b)
+        if (T.slot6[v * 32u + b].id != ID6_EMPTY) bits |= 1u << b;
+      T.occ6[v] = bits;
+    }
   }
 }
 
@@ -328,8 +320,8 @@ extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int oo_table_launch_fp(const oo_rx::DevTables* T, hipStream_t s) {
-  hipLaunchKernelGGL(oo_rx::table_fp, dim3(grid_for(T->ip4_mask + T->ip6_mask + 2u)), dim3(256), 0,
-                     s, *T);
+extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s) {
+  hipLaunchKernelGGL(oo_rx::table_occ, dim3(grid_for((T->ip4_mask + T->ip6_mask + 2u) / 32u + 2u)),
+                     dim3(256), 0, s, *T);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -73,18 +73,3 @@ def test_store_counts(asm):
     assert not re.findall(r"global_store_(byte|dword\b|dwordx2)", tx)
     for body in (rx, tx):  # flat stores would count in lgkmcnt as well
         assert not re.findall(r"flat_store|flat_load|flat_atomic", body)
-
-
-def test_asm_sgpr_base_hazard(asm):
-    """Inline-asm vector loads that take an SGPR base (the demux's table
-    loads) open with s_nop 4: the base is often reloaded by v_readlane (a VALU
-    write of an SGPR) right before the block, a VMEM read of that SGPR needs 5
-    wait states, and the compiler pads only its own instructions.  Without
-    them the load used a stale base and faulted."""
-    text, _ = asm
-    blocks = re.findall(r";;#ASMSTART\n(.*?);;#ASMEND", text, re.S)
-    based = [b for b in blocks if re.search(r"global_load\w*\s+v\S+,\s*v\d+,\s*s\[", b)]
-    assert based, "no SGPR-based asm loads found"
-    for b in based:
-        first = [ln.strip() for ln in b.splitlines() if ln.strip()][0]
-        assert first == "s_nop 4", b
