@@ -83,7 +83,7 @@ enum {
 #define OO_RX_F_CSUM_OK 0x04u  /* L3+L4 software checksum verified                */
 #define OO_RX_F_MCAST   0x08u  /* daddr multicast/broadcast: host must keep
                                   delivering to every match (udp_rx.c:148-203)     */
-#define OO_RX_F_MULTI   0x10u  /* nmatch > 1 in the deciding stage               */
+#define OO_RX_F_MULTI   0x10u  /* nmatch > 1 in the deciding stage (UDP only)    */
 #define OO_RX_F_TSO     0x20u  /* TCP header in the timestamp-option fast layout
                                   (doff 8, options NOP NOP TS 10: tcp_rx.c:4537-4543,
                                   CI_TCP_TSO_WORD ip_shared_types.h:2742); the host
@@ -126,7 +126,8 @@ typedef struct oo_gpu_rx_result {
   uint16_t ip_paylen;   /* IPv4 tot_len-4*IHL / IPv6 payload_len             */
   uint16_t sport_be;    /* L4 source port, network order in host integer     */
   uint16_t dport_be;    /* L4 dest port                                      */
-  uint16_t nmatch;      /* matching filter entries in the deciding stage     */
+  uint16_t nmatch;      /* matching filter entries in the deciding stage;
+                           TCP: 1 (its walk ends at the first match)         */
   uint32_t saddr_be;    /* IPv4 saddr / IPv6 addr xor-fold                   */
   uint32_t daddr_be;    /* IPv4 daddr / IPv6 addr xor-fold                   */
   int32_t  sock;        /* matched socket id (OO_SP) or -1                   */

@@ -387,12 +387,16 @@ __device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool f
 // (occ_next), and -- when have -- the first slot's record: the common walk
 // (an EMPTY first slot, or one occupied slot followed by an EMPTY one) needs
 // no more loads.  Tombstones continue the walk; an EMPTY slot or a full
-// cycle ends it.
+// cycle ends it, and so does the first match when stop: TCP's deliver
+// callbacks always return 1 (tcp_rx.c:4644-4657), which ends the reference's
+// walk there (handle_entry, netif_table.c:225-229); UDP counts every match
+// (ci_udp_rx_deliver continues past a multicast destination or a socket
+// that drops, udp_rx.c:194-228).
 template <bool IS6>
 __device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_t la[4],
                       uint32_t lp, const uint32_t ra[4], bool ra_null, uint32_t rp, uint32_t proto,
                       int intf_i, int vlan, uint32_t h1, uint32_t h2, bool occ, Rec rec, bool have,
-                      bool occ_next) {
+                      bool occ_next, bool stop) {
   Match m = {-1, 0};
   const uint32_t first = h1;
   if (occ && !have) rec = load_rec(P, t, h1, any6);  // the first slot's record was not preloaded
@@ -402,6 +406,7 @@ __device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_
     if (rec_match<IS6>(P, rec, guard == 0, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id)) {
       if (m.n == 0) m.first = id;
       ++m.n;
+      if (stop) break;
     }
     h1 = (h1 + h2) & t.mask;
     if (h1 == first) break;
@@ -871,16 +876,16 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
   const uint32_t dx = IS6 ? (h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3]) : h.da[0];
   const uint32_t sx = IS6 ? (h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3]) : h.sa[0];
   Match m = walk<IS6>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
-                      hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0);
+                      hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0, tcp);
   stage = 1;
   if (m.n == 0) {
     m = walk<IS6>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
-                  hash2(dx, dport, 0u, 0u, proto), o1, rec, fs == 1, q1);
+                  hash2(dx, dport, 0u, 0u, proto), o1, rec, fs == 1, q1, tcp);
     stage = 2;
   }
   if (m.n == 0 && tcp) {
     m = walk<IS6>(P, t, any6, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2,
-                  hash2(0u, dport, 0u, 0u, proto), o2, rec, fs == 2, q2);
+                  hash2(0u, dport, 0u, 0u, proto), o2, rec, fs == 2, q2, true);
     stage = 3;
   }
   return m;

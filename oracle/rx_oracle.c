@@ -581,11 +581,15 @@ static inline int bind2dev_ok(const oo_or_tables* t, const oo_gpu_rx_sock* s,
          s->bind2dev_vlan == vlan;
 }
 
-/* ci_netif_filter_for_each_match (netif_table.c:234-319) with a callback
- * that accepts nothing, so the walk runs to its end. */
+/* ci_netif_filter_for_each_match (netif_table.c:234-319).  stop: the
+ * callback ends the walk at the first match (handle_entry, :225-229) -- TCP's
+ * ci_tcp_rx_deliver_to_conn / _to_listen always return 1 (tcp_rx.c:
+ * 4644-4657); otherwise (UDP, whose ci_udp_rx_deliver continues past a
+ * multicast destination or a socket that drops, udp_rx.c:194-228) every
+ * match is counted and the walk runs to its end. */
 static match_t walk4(const oo_or_tables* t, uint32_t la, uint32_t lp,
                      uint32_t ra, uint32_t rp, uint32_t proto, int intf_i,
-                     int vlan)
+                     int vlan, int stop)
 {
   match_t m = { -1, 0 };
   uint32_t h1 = oo_or_hash1(t->ip4_mask, la, lp, ra, rp, proto);
@@ -601,6 +605,8 @@ static match_t walk4(const oo_or_tables* t, uint32_t la, uint32_t lp,
           bind2dev_ok(t, s, intf_i, vlan) ) {
         if( m.n++ == 0 )
           m.first = (int32_t)(st & ID_MASK);
+        if( stop )
+          break;
       }
     }
     if( (st & ST_MASK) == ST_EMPTY )
@@ -616,10 +622,11 @@ static match_t walk4(const oo_or_tables* t, uint32_t la, uint32_t lp,
   return m;
 }
 
-/* ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189). */
+/* ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189); stop as
+ * in walk4. */
 static match_t walk6(const oo_or_tables* t, const uint8_t* la, uint32_t lp,
                      const uint8_t* ra /* NULL = [::] */, uint32_t rp,
-                     uint32_t proto, int intf_i, int vlan)
+                     uint32_t proto, int intf_i, int vlan, int stop)
 {
   match_t m = { -1, 0 };
   uint32_t lx = oo_or_addr_xor(la), rx = oo_or_addr_xor(ra);
@@ -636,6 +643,8 @@ static match_t walk6(const oo_or_tables* t, const uint8_t* la, uint32_t lp,
           bind2dev_ok(t, s, intf_i, vlan) ) {
         if( m.n++ == 0 )
           m.first = id;
+        if( stop )
+          break;
       }
     }
     else if( id == ID6_EMPTY )
@@ -841,18 +850,18 @@ void oo_or_rx_one(const oo_or_tables* t, const uint8_t* frame, int len,
       const uint8_t* da = frame + l3 + 24;
       r->hash3 = oo_or_hash3(oo_or_addr_xor(da), dport, oo_or_addr_xor(sa),
                              sport, proto);
-      m[0] = walk6(t, da, dport, sa, sport, proto, intf_i, vlan);
-      m[1] = walk6(t, da, dport, NULL, 0, proto, intf_i, vlan);
+      m[0] = walk6(t, da, dport, sa, sport, proto, intf_i, vlan, nst == 3);
+      m[1] = walk6(t, da, dport, NULL, 0, proto, intf_i, vlan, nst == 3);
       if( nst == 3 )
-        m[2] = walk6(t, zero16, dport, NULL, 0, proto, intf_i, vlan);
+        m[2] = walk6(t, zero16, dport, NULL, 0, proto, intf_i, vlan, 1);
     }
     else {
       uint32_t sa = r->saddr_be, da = r->daddr_be;
       r->hash3 = oo_or_hash3(da, dport, sa, sport, proto);
-      m[0] = walk4(t, da, dport, sa, sport, proto, intf_i, vlan);
-      m[1] = walk4(t, da, dport, 0, 0, proto, intf_i, vlan);
+      m[0] = walk4(t, da, dport, sa, sport, proto, intf_i, vlan, nst == 3);
+      m[1] = walk4(t, da, dport, 0, 0, proto, intf_i, vlan, nst == 3);
       if( nst == 3 )
-        m[2] = walk4(t, 0, dport, 0, 0, proto, intf_i, vlan);
+        m[2] = walk4(t, 0, dport, 0, 0, proto, intf_i, vlan, 1);
     }
     if( proto == 17 ) {
       /* ci_udp_rx_deliver's multi-destination test reads the IPv4 view of
