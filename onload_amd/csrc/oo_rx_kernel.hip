@@ -332,9 +332,12 @@ __device__ __forceinline__ Rec load_rec(const KParams& P, const Probe& t, uint32
   r.d0 = gload16(a);
   r.d1 = gload16(a + 16u);
   r.d2 = r.d3 = make_uint4(0, 0, 0, 0);
-  if (any6 && t.is6) {
-    r.d2 = gload16(a + 32u);
-    r.d3 = gload16(a + 48u);
+  if (any6) {
+    // No branch (one would end in a wait for the loads above): an IPv4
+    // lane reads its first half again and ignores it.
+    const uint64_t b = t.is6 ? a + 32u : a;
+    r.d2 = gload16(b);
+    r.d3 = gload16(b + 16u);
   }
   return r;
 }
@@ -380,6 +383,23 @@ __device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool f
   return ok && bind2dev_ok(P, sflags, hw, b2d, intf_i, vlan);
 }
 
+// One slot against the lookup key for a lane of either family: M = 0 IPv4,
+// 1 IPv6, 2 per lane (t.is6) -- both compares, no loads, so a wave holding
+// both families walks in one instruction stream.
+template <int M>
+__device__ __forceinline__ bool rec_match_m(const KParams& P, const Probe& t, const Rec& r,
+                                            bool first4, const uint32_t la[4], uint32_t lp,
+                                            const uint32_t ra[4], bool ra_null, uint32_t rp,
+                                            uint32_t proto, int intf_i, int vlan, int32_t& id) {
+  if (M == 0) return rec_match<false>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id);
+  if (M == 1) return rec_match<true>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id);
+  int32_t id4, id6;
+  const bool m4 = rec_match<false>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id4);
+  const bool m6 = rec_match<true>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id6);
+  id = t.is6 ? id6 : id4;
+  return t.is6 ? m6 : m4;
+}
+
 // ci_netif_filter_for_each_match (netif_table.c:234-319) /
 // ci_netif_filter_for_each_match_ip6 (netif_table_ip6.c:110-189) over the
 // slot records, every match counted.  The caller has loaded the not-EMPTY
@@ -392,7 +412,7 @@ __device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool f
 // walk there (handle_entry, netif_table.c:225-229); UDP counts every match
 // (ci_udp_rx_deliver continues past a multicast destination or a socket
 // that drops, udp_rx.c:194-228).
-template <bool IS6>
+template <int M>
 __device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_t la[4],
                       uint32_t lp, const uint32_t ra[4], bool ra_null, uint32_t rp, uint32_t proto,
                       int intf_i, int vlan, uint32_t h1, uint32_t h2, bool occ, Rec rec, bool have,
@@ -403,7 +423,7 @@ __device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_
   for (uint32_t guard = 0; guard <= t.mask; ++guard) {
     if (!occ) break;  // an EMPTY slot ends the walk
     int32_t id;
-    if (rec_match<IS6>(P, rec, guard == 0, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id)) {
+    if (rec_match_m<M>(P, t, rec, guard == 0, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id)) {
       if (m.n == 0) m.first = id;
       ++m.n;
       if (stop) break;
@@ -864,8 +884,10 @@ __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, u
 }
 
 // The 2 (UDP) or 3 (TCP) lookup stages of one lane in reference order; the
-// first stage with a match decides (*stage = 1..3).
-template <bool IS6>
+// first stage with a match decides (*stage = 1..3).  M as rec_match_m: a wave
+// holding both families walks them together (M = 2), so its walks cost the
+// dependent loads of one family, not of both in turn.
+template <int M>
 __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t, bool any6,
                                                const Hdr& h, uint32_t dport, uint32_t sport,
                                                uint32_t proto, int intf_i, int vlan, bool tcp,
@@ -873,18 +895,19 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
                                                bool o0, bool o1, bool o2, bool q0, bool q1,
                                                bool q2, Rec rec, int fs, int& stage) {
   const uint32_t zero[4] = {0, 0, 0, 0};
-  const uint32_t dx = IS6 ? (h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3]) : h.da[0];
-  const uint32_t sx = IS6 ? (h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3]) : h.sa[0];
-  Match m = walk<IS6>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
+  const bool six = M == 1 || (M == 2 && t.is6);
+  const uint32_t dx = six ? (h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3]) : h.da[0];
+  const uint32_t sx = six ? (h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3]) : h.sa[0];
+  Match m = walk<M>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
                       hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0, tcp);
   stage = 1;
   if (m.n == 0) {
-    m = walk<IS6>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
+    m = walk<M>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
                   hash2(dx, dport, 0u, 0u, proto), o1, rec, fs == 1, q1, tcp);
     stage = 2;
   }
   if (m.n == 0 && tcp) {
-    m = walk<IS6>(P, t, any6, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2,
+    m = walk<M>(P, t, any6, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2,
                   hash2(0u, dport, 0u, 0u, proto), o2, rec, fs == 2, q2, true);
     stage = 3;
   }
@@ -977,15 +1000,11 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
         const uint32_t dd = is6 ? h.sa[2] : h.da[0];
         if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
       }
-      // The walks compare per address family (divergent only in waves that
-      // hold both): the loads above were shared.
-      Match m;
+      // Both families walk in one instruction stream (lookup_stages<2>).
       int stage;
-      if (ANY6 && is6) m = lookup_stages<true>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp,
-                                               h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs,
-                                               stage);
-      else m = lookup_stages<false>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0,
-                                    h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
+      const Match m = lookup_stages<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, intf_i, vlan,
+                                                  tcp, h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2,
+                                                  rec, fs, stage);
       DSTAMP(10);
       reason = OO_RX_R_NO_MATCH;
       if (m.n) {
