@@ -887,7 +887,7 @@ __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, u
 // first stage with a match decides (*stage = 1..3).  M as rec_match_m: a wave
 // holding both families walks them together (M = 2), so its walks cost the
 // dependent loads of one family, not of both in turn.
-template <int M>
+template <int M, bool PRE1>
 __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t, bool any6,
                                                const Hdr& h, uint32_t dport, uint32_t sport,
                                                uint32_t proto, int intf_i, int vlan, bool tcp,
@@ -898,12 +898,19 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
   const bool six = M == 1 || (M == 2 && t.is6);
   const uint32_t dx = six ? (h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3]) : h.da[0];
   const uint32_t sx = six ? (h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3]) : h.sa[0];
+  // Stage 2's first record, when stage 1 did not get the up-front one, is
+  // loaded beside stage 1's walk (ready when that walk ends without a match,
+  // instead of one more dependent load after it).  PRE1: IPv4-only waves --
+  // a second 64-B record in a wave holding IPv6 spills.
+  Rec rec1 = rec;
+  const bool pre1 = PRE1 && fs == 0 && o1;
+  if (pre1) rec1 = load_rec(P, t, h1_1, any6);
   Match m = walk<M>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
                       hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0, tcp);
   stage = 1;
   if (m.n == 0) {
     m = walk<M>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
-                  hash2(dx, dport, 0u, 0u, proto), o1, rec, fs == 1, q1, tcp);
+                  hash2(dx, dport, 0u, 0u, proto), o1, rec1, fs == 1 || pre1, q1, tcp);
     stage = 2;
   }
   if (m.n == 0 && tcp) {
@@ -930,35 +937,17 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
   uint32_t flags = h.flags;
   const bool is6 = h.is6;
 
-  oo_gpu_rx_result r;
-  r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
-  r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
-  r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
-  if (h.l3ok) {
-    r.proto = (uint8_t)proto;
-    r.ip_paylen = (uint16_t)h.ip_paylen;
-  }
-  // Lanes that reach the lookups.
-  bool look = false;
-  if (reason == PENDING) {
-    flags |= OO_RX_F_CSUM_OK;
-    r.l4_off = (uint16_t)h.l4;
-    r.sport_be = (uint16_t)h.sport;
-    r.dport_be = (uint16_t)h.dport;
-    if (is6) {
-      r.saddr_be = h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3];
-      r.daddr_be = h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3];
-    } else {
-      r.saddr_be = h.sa[0];
-      r.daddr_be = h.da[0];
-    }
-    reason = h.late;
-    look = reason == PENDING;
-  }
+  // Lanes that reach the lookups.  The record is assembled after them: its
+  // fields come from the headers, which the lookups hold anyway.
+  const bool csum_ok = reason == PENDING;
+  const bool look = csum_ok && h.late == PENDING;
+  const uint32_t sport = h.sport, dport = h.dport;
+  const uint32_t sx = is6 ? h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3] : h.sa[0];  // hash addresses
+  const uint32_t dx = is6 ? h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3] : h.da[0];
+  Match m = {-1, 0};
+  int stage = 0;
   if (__ballot(look) != 0) {
     constexpr bool any6 = ANY6;
-    const uint32_t sport = h.sport, dport = h.dport;
-    const uint32_t dx = r.daddr_be, sx = r.saddr_be;  // hash addresses
     const Probe t = probe_of(P, ANY6 && is6);
     const bool tcp = proto == 6u;
     const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & t.mask;
@@ -992,28 +981,45 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     if (look && fs < 3) rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
     if (look) {
       DSTAMP(9);
-      r.hash3 = hash3(dx, dport, sx, sport, proto);
-      if (proto == 17u) {
-        // ci_udp_rx_deliver's multi-destination test reads the IPv4 view
-        // of the L3 header (udp_rx.c:157-159): bytes 16..19, which for
-        // IPv6 are source-address bytes 8..11.
-        const uint32_t dd = is6 ? h.sa[2] : h.da[0];
-        if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
-      }
       // Both families walk in one instruction stream (lookup_stages<2>).
-      int stage;
-      const Match m = lookup_stages<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, intf_i, vlan,
-                                                  tcp, h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2,
-                                                  rec, fs, stage);
+      m = lookup_stages<ANY6 ? 2 : 0, !ANY6>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0,
+                                      h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
       DSTAMP(10);
-      reason = OO_RX_R_NO_MATCH;
-      if (m.n) {
-        reason = OO_RX_R_DELIVER;
-        r.stage = (uint8_t)stage;
-        r.sock = m.first;
-        r.nmatch = (uint16_t)m.n;
-        if (m.n > 1) flags |= OO_RX_F_MULTI;
-      }
+    }
+  }
+  oo_gpu_rx_result r;
+  r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
+  r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;
+  r.saddr_be = 0; r.daddr_be = 0; r.sock = -1; r.hash3 = 0;
+  if (h.l3ok) {
+    r.proto = (uint8_t)proto;
+    r.ip_paylen = (uint16_t)h.ip_paylen;
+  }
+  if (csum_ok) {
+    flags |= OO_RX_F_CSUM_OK;
+    r.l4_off = (uint16_t)h.l4;
+    r.sport_be = (uint16_t)sport;
+    r.dport_be = (uint16_t)dport;
+    r.saddr_be = sx;
+    r.daddr_be = dx;
+    reason = h.late;
+  }
+  if (look) {
+    r.hash3 = hash3(dx, dport, sx, sport, proto);
+    if (proto == 17u) {
+      // ci_udp_rx_deliver's multi-destination test reads the IPv4 view of
+      // the L3 header (udp_rx.c:157-159): bytes 16..19, which for IPv6 are
+      // source-address bytes 8..11.
+      const uint32_t dd = is6 ? h.sa[2] : h.da[0];
+      if ((dd & 0xf0u) == 0xe0u || dd == 0xffffffffu) flags |= OO_RX_F_MCAST;
+    }
+    reason = OO_RX_R_NO_MATCH;
+    if (m.n) {
+      reason = OO_RX_R_DELIVER;
+      r.stage = (uint8_t)stage;
+      r.sock = m.first;
+      r.nmatch = (uint16_t)m.n;
+      if (m.n > 1) flags |= OO_RX_F_MULTI;
     }
   }
   r.reason = (uint8_t)reason;
