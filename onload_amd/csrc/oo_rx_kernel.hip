@@ -907,12 +907,14 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
   if (pre1) rec1 = load_rec(P, t, h1_1, any6);
   Match m = walk<M>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
                       hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0, tcp);
+  DSTAMP(11);
   stage = 1;
   if (m.n == 0) {
     m = walk<M>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
                   hash2(dx, dport, 0u, 0u, proto), o1, rec1, fs == 1 || pre1, q1, tcp);
     stage = 2;
   }
+  DSTAMP(12);
   if (m.n == 0 && tcp) {
     m = walk<M>(P, t, any6, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2,
                   hash2(0u, dport, 0u, 0u, proto), o2, rec, fs == 2, q2, true);

@@ -88,8 +88,9 @@ def main() -> None:
         "rounds_mean": float(ph[:, 7].mean()),
         "stream_ns_per_round": float((d(3, 4) / np.maximum(ph[:, 7], 1)).mean()),
     }
-    # Inside the demux (slots 8-10, when the build stamps them): first-probe
-    # occupancy words landed, first records issued, stages walked.
+    # Inside the demux (slots 8-12, when the build stamps them): first-probe
+    # occupancy words landed, first records issued, stages walked (11, 12:
+    # after the first and the second stage).
     dm = ph[:, 8] != 0
     if dm.any():
         q = ph[dm]
@@ -97,6 +98,13 @@ def main() -> None:
                                 "to_walks": float(((q[:, 9] - q[:, 8]) * ns).mean() / 1e3),
                                 "walks": float(((q[:, 10] - q[:, 9]) * ns).mean() / 1e3),
                                 "after_walks": float(((q[:, 3] - q[:, 10]) * ns).mean() / 1e3)}
+        # Per stage (slots 11, 12: after the first and second stage walks).
+        st = dm & (ph[:, 9] != 0) & (ph[:, 10] != 0) & (ph[:, 11] != 0) & (ph[:, 12] != 0)
+        if st.any():
+            q = ph[st]
+            res["walk_stage_us_mean"] = [float(((q[:, 11] - q[:, 9]) * ns).mean() / 1e3),
+                                         float(((q[:, 12] - q[:, 11]) * ns).mean() / 1e3),
+                                         float(((q[:, 10] - q[:, 12]) * ns).mean() / 1e3)]
     # Phase concurrency over time: the fraction of live waves streaming a
     # body (stamps 3 -> 4) vs in the header phases (0 -> 3), in 1-us bins --
     # synchronised header phases show as dips in the streaming fraction.
