@@ -185,22 +185,25 @@ def run_rank(args) -> None:
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # One HIP event pair on the launch stream around the K back-to-back
+    # launches: kernel time = region / K (an event pair around every launch
+    # would add the event and dispatch gap to each one: ~7 us on a 265-us
+    # kernel, against the rocprofv3 duration).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        e.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t_end = time.perf_counter()
     local_ms = (t_end - t_start) * 1e3 / args.steps
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = float(ev0.elapsed_time(ev1)) / args.steps
     if world > 1:
         t = torch.tensor([local_ms, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -350,18 +353,8 @@ def time_tx_fill(torch, stack, frames, d_desc, n, mean_len, sh, steps, warmup):
     """The TX checksum fill over the same HBM-resident frames (in place; a
     fill of already-filled frames rewrites the same values).  Algorithmic
     bytes: the frame read, the descriptor, the 4 check-field bytes written."""
-    for _ in range(warmup):
-        stack.tx_fill_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n, sh)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
-    stream = torch.cuda.current_stream()
-    torch.cuda.synchronize()
-    for s, e in ev:
-        s.record(stream)
-        stack.tx_fill_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n, sh)
-        e.record(stream)
-    torch.cuda.synchronize()
-    ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    ms = _timed(torch, lambda: stack.tx_fill_dev(frames.data_ptr(), frames.numel(),
+                                                 d_desc.data_ptr(), n, sh), steps, warmup)
     bpp = mean_len + DESC_B + 4
     gbs = n * bpp / (ms * 1e-3) / 1e9
     return {"kernel_ms": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 1),
@@ -403,16 +396,16 @@ def _ring(addr, lens, cons):
 def _timed(torch, run, steps, warmup):
     for _ in range(warmup):
         run()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+    # one event pair around the back-to-back launches (as the main timing)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     stream = torch.cuda.current_stream()
     torch.cuda.synchronize()
-    for s, e in ev:
-        s.record(stream)
+    ev0.record(stream)
+    for _ in range(steps):
         run()
-        e.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
-    return float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    return float(ev0.elapsed_time(ev1)) / steps
 
 
 def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=256):

@@ -197,9 +197,17 @@ __device__ uint64_t* dstamp_slot(uint64_t* p = nullptr, bool set = false) {
     if (dp_ != nullptr && __builtin_amdgcn_mbcnt_lo(~0u, 0u) == 0)                    \
       dp_[(ph)] = __builtin_amdgcn_s_memrealtime();                                   \
   } while (0)
+#define DSTAMPV(ph, v)                                                                \
+  do {                                                                                \
+    uint64_t* dp_ = dstamp_slot();                                                    \
+    if (dp_ != nullptr && __builtin_amdgcn_mbcnt_lo(~0u, 0u) == 0) dp_[(ph)] = (v);   \
+  } while (0)
 #else
 #define DSTAMP(ph) \
   do {             \
+  } while (0)
+#define DSTAMPV(ph, v) \
+  do {                 \
   } while (0)
 #define STAMP(ph, val) \
   do {                 \
@@ -923,6 +931,91 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
   return m;
 }
 
+// The same lookups as one per-lane state machine (OO_RX_FSM): every step
+// each live lane evaluates the slot whose record it holds, advances along
+// its stage's probe sequence or on to its next stage (stages whose first
+// slot is EMPTY, and a second slot known EMPTY, are passed without a load),
+// and loads the next record it needs -- one dependent load per step for the
+// whole wave.  The sequential walks cost a wave the sum over stages of its
+// longest walk in each; this costs the longest per-lane total (config 5:
+// 7.5 against 4.6 slot visits per 64 packets, tools/walk_levels.py).
+#ifndef OO_RX_FSM
+#define OO_RX_FSM 1
+#endif
+template <int M>
+__device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bool any6,
+                                            const Hdr& h, uint32_t dport, uint32_t sport,
+                                            uint32_t proto, int intf_i, int vlan, bool tcp,
+                                            uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
+                                            uint32_t h2_0, uint32_t h2_1, uint32_t h2_2, bool o0,
+                                            bool o1, bool o2, bool q0, bool q1, bool q2, Rec rec,
+                                            int fs, int& stage) {
+  const uint32_t nst = tcp ? 3u : 2u;  // o2 (and q2) are false for UDP
+  (void)o0;
+  Match m = {-1, 0};
+  uint32_t s = (uint32_t)fs;  // the first stage whose first slot is occupied (3: none)
+  bool live = s < nst;
+  uint32_t h1 = s == 0 ? h1_0 : s == 1 ? h1_1 : h1_2;
+  uint32_t first = h1;
+  uint32_t h2 = s == 0 ? h2_0 : s == 1 ? h2_1 : h2_2;
+  uint32_t k = 0;    // probe index within the stage
+  bool occ = true;   // slot h1 not EMPTY (rec is its record)
+  uint32_t guard = 0;
+  for (; __ballot(live) != 0 && guard <= 3u * (t.mask + 1u); ++guard) {
+    if (live) {
+      // The slot in hand (netif_table.c:192-231 / netif_table_ip6.c:146-170).
+      bool end = !occ;  // an EMPTY slot ends the stage's walk
+      if (occ) {
+        const bool st0 = s == 0;
+        uint32_t la[4], ra[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          la[i] = s < 2 ? h.da[i] : 0u;
+          ra[i] = st0 ? h.sa[i] : 0u;
+        }
+        int32_t id;
+        if (rec_match_m<M>(P, t, rec, k == 0, la, dport, ra, !st0, st0 ? sport : 0u, proto,
+                           intf_i, vlan, id)) {
+          if (m.n == 0) m.first = id;
+          ++m.n;
+          end = tcp;  // TCP's deliver callbacks end the walk at the first match
+        }
+        if (!end) {
+          h1 = (h1 + h2) & t.mask;
+          end = h1 == first;  // a full cycle
+          ++k;
+          // the second slot's bit came with the first batch
+          if (!end && k == 1) end = !(s == 0 ? q0 : s == 1 ? q1 : q2);
+        }
+      }
+      if (end) {
+        if (m.n != 0) {
+          live = false;  // this stage decides
+          stage = (int)s + 1;
+        } else {
+          // on to the next stage whose first slot is occupied
+          ++s;
+          if (s == 1 && !o1) ++s;
+          if (s == 2 && !o2) ++s;
+          live = s < nst;
+          h1 = s == 1 ? h1_1 : h1_2;
+          first = h1;
+          h2 = s == 1 ? h2_1 : h2_2;
+          k = 0;
+        }
+      }
+      // The next record (and, past the second slot, its occupancy bit with
+      // it: an EMPTY slot's record is simply not used).
+      if (live) {
+        rec = load_rec(P, t, h1, any6);
+        occ = k < 2 ? true : probe_occ(P, t, h1);
+      }
+    }
+  }
+  DSTAMPV(11, 1000000u + guard);  // the wave's steps (marked: not a time)
+  return m;
+}
+
 // The record of one packet from its headers: the lookup stages of
 // ci_udp_handle_rx (udp_rx.c:271-306: full 4-tuple, then (laddr, lport)) or
 // ci_tcp_handle_rx (tcp_rx.c:4786-4835: then (*, lport)); the first stage
@@ -984,8 +1077,14 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     if (look) {
       DSTAMP(9);
       // Both families walk in one instruction stream (lookup_stages<2>).
-      m = lookup_stages<ANY6 ? 2 : 0, !ANY6>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0,
-                                      h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
+      // Waves with TCP lookups (three stages, long connected-socket chains)
+      // take the state machine; UDP-only waves the stage-by-stage walks.
+      if (OO_RX_FSM && __ballot(tcp) != 0)
+        m = lookup_fsm<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0, h1_1,
+                                     h1_2, h2_0, h2_1, h2_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
+      else
+        m = lookup_stages<ANY6 ? 2 : 0, !ANY6>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp,
+                                               h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
       DSTAMP(10);
     }
   }

@@ -98,8 +98,13 @@ def main() -> None:
                                 "to_walks": float(((q[:, 9] - q[:, 8]) * ns).mean() / 1e3),
                                 "walks": float(((q[:, 10] - q[:, 9]) * ns).mean() / 1e3),
                                 "after_walks": float(((q[:, 3] - q[:, 10]) * ns).mean() / 1e3)}
+        # The state-machine walk stamps its step count in slot 11 (+1e6).
+        fsm = dm & (ph[:, 11] >= 1000000) & (ph[:, 11] < 2000000)
+        if fsm.any():
+            res["fsm_steps_mean"] = float((ph[fsm, 11] - 1000000).mean())
+            res["fsm_steps_hist"] = np.bincount((ph[fsm, 11] - 1000000).astype(np.int64)).tolist()
         # Per stage (slots 11, 12: after the first and second stage walks).
-        st = dm & (ph[:, 9] != 0) & (ph[:, 10] != 0) & (ph[:, 11] != 0) & (ph[:, 12] != 0)
+        st = dm & (ph[:, 11] < 1000000) & (ph[:, 9] != 0) & (ph[:, 10] != 0) & (ph[:, 11] != 0) & (ph[:, 12] != 0)
         if st.any():
             q = ph[st]
             res["walk_stage_us_mean"] = [float(((q[:, 11] - q[:, 9]) * ns).mean() / 1e3),
