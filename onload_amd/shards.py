@@ -7,8 +7,12 @@ collective touches the data path.  What does move between ranks:
 
 * the filter tables: built once on rank 0 (the stack that owns the socket
   world), broadcast as one table image (oo_gpu_rx_table_export / _import,
-  ~3.4 MB at the default sizes) over RCCL, then kept current by every rank
-  applying the same filter ops (the ops are deterministic);
+  ~3.4 MB at the default sizes) over RCCL, then kept current incrementally:
+  rank 0 broadcasts each batch of filter ops (insert / remove / socket
+  fields, 96 B each, broadcast_ops) and every rank applies it in order --
+  the ops are deterministic, so the tables stay identical, return codes
+  included (`oof` applies its deferred ops at the same serialisation point,
+  oof_interface.c:184-217);
 * optionally the frames, when they arrive on one ingest GPU: a scatter;
 * optionally the 32-B records, gathered back to one rank.
 
@@ -78,6 +82,73 @@ def broadcast_tables(stack, torch, dist, device, src: int = 0, stream: int = 0) 
     return nbytes
 
 
+#: one filter-table op as it travels between ranks
+OP_INSERT, OP_REMOVE, OP_SOCK = 0, 1, 2
+OP_DTYPE = np.dtype([("kind", "u1"), ("af", "u1"), ("proto", "u1"), ("raddr_any", "u1"),
+                     ("lport_be", "<u2"), ("rport_be", "<u2"), ("sock", "<i4"), ("rsvd", "<u4"),
+                     ("laddr", "u1", 16), ("raddr", "u1", 16), ("fields", "u1", 48)])
+assert OP_DTYPE.itemsize == 96
+
+
+def pack_ops(ops) -> np.ndarray:
+    """Filter-table ops as OP_DTYPE records.  An op is
+    ("insert" | "remove", sock_id, af, laddr bytes, lport_be, raddr bytes | None,
+    rport_be, proto) -- ci_netif_filter_insert / _remove's arguments -- or
+    ("sock", sock_id, _abi.Sock) -- the socket fields the demux reads."""
+    out = np.zeros(len(ops), dtype=OP_DTYPE)
+    for i, o in enumerate(ops):
+        r = out[i]
+        if o[0] == "sock":
+            r["kind"], r["sock"] = OP_SOCK, o[1]
+            r["fields"] = np.frombuffer(bytes(o[2]), dtype=np.uint8)
+            continue
+        kind, sock, af, la, lport_be, ra, rport_be, proto = o
+        r["kind"] = OP_INSERT if kind == "insert" else OP_REMOVE
+        r["sock"], r["af"], r["proto"] = sock, af, proto
+        r["lport_be"], r["rport_be"] = lport_be, rport_be
+        r["laddr"][: len(la)] = np.frombuffer(la, dtype=np.uint8)
+        if ra is None:
+            r["raddr_any"] = 1
+        else:
+            r["raddr"][: len(ra)] = np.frombuffer(ra, dtype=np.uint8)
+    return out
+
+
+def apply_ops(stack, recs: np.ndarray) -> list[int]:
+    """Applies packed ops to a stack in order; returns their return codes."""
+    rcs = []
+    for r in recs:
+        kind = int(r["kind"])
+        if kind == OP_SOCK:
+            rcs.append(stack.sock_set(int(r["sock"]), _abi.Sock.from_buffer_copy(r["fields"].tobytes())))
+            continue
+        n = 4 if int(r["af"]) == 4 else 16
+        la = r["laddr"][:n].tobytes()
+        ra = None if r["raddr_any"] else r["raddr"][:n].tobytes()
+        f = stack.filter_insert_raw if kind == OP_INSERT else stack.filter_remove_raw
+        rc = f(int(r["sock"]), int(r["af"]), la, int(r["lport_be"]), ra, int(r["rport_be"]),
+               int(r["proto"]))
+        rcs.append(0 if rc is None else int(rc))
+    return rcs
+
+
+def broadcast_ops(stack, ops, torch, dist, device, src: int = 0) -> list[int]:
+    """One incremental table update on every rank: rank src packs its ops
+    (pack_ops), one broadcast of the count and one of the records, and every
+    rank -- src too -- applies them in order (apply_ops).  Other ranks pass
+    ops=None.  Returns this rank's return codes (identical on every rank)."""
+    cnt = torch.tensor([len(ops) if dist.get_rank() == src else 0], dtype=torch.int64,
+                       device=device)
+    dist.broadcast(cnt, src=src)
+    n = int(cnt.item())
+    buf = torch.zeros(n * OP_DTYPE.itemsize, dtype=torch.uint8, device=device)
+    if dist.get_rank() == src and n:
+        buf.copy_(torch.from_numpy(pack_ops(ops).view(np.uint8)))
+    if n:
+        dist.broadcast(buf, src=src)
+    return apply_ops(stack, buf.cpu().numpy().view(OP_DTYPE))
+
+
 def gather_records(records, count: int, torch, dist, dst: int = 0):
     """Gather every rank's records (a uint8 tensor of >= 32*count bytes) on
     rank dst in rank order; ranks may hold different counts.  Returns the
@@ -128,4 +199,5 @@ def host_cores() -> int:
 
 
 __all__ = ["shard_range", "split_bytes", "shard_for", "broadcast_tables", "gather_records",
-           "scatter_frames", "host_cores", "MIXED_CONFIGS"]
+           "scatter_frames", "host_cores", "MIXED_CONFIGS", "pack_ops", "apply_ops",
+           "broadcast_ops", "OP_DTYPE"]

@@ -4,7 +4,8 @@ helpers the GPU run uses (onload_amd/shards.py):
 
 * shards: contiguous ranges covering the stream exactly, byte-balanced for
   the mixed-size configurations;
-* the table image broadcast from rank 0 replicates its tables on rank 1;
+* the table image broadcast from rank 0 replicates its tables on rank 1,
+  and incremental op batches from rank 0 keep them identical;
 * per-rank records gathered to rank 0 equal one unsharded run, bit for bit;
 * the frame scatter delivers each rank its own shard;
 * bench.py --gpus N starts N ranks itself (WORLD_SIZE=N, before anything
@@ -106,6 +107,79 @@ def test_two_rank_shards_equal_one_run(config):
     want = o.handle_rx_batch(buf, desc)
     assert recs == want.tobytes()
     np.testing.assert_array_equal(ctr, counters_of(want))
+
+
+def _ops_worker(rank, world, port, q):
+    """Image broadcast after the first part of a table script, then the rest
+    of it as incremental op batches from rank 0 (shards.broadcast_ops)."""
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import table_scripts as ts
+    from onload_amd.rx import GpuRxStack
+    cfg, socks, ops = ts.build("mixed")
+    ops = [o for o in ops if o[0] in "AR"]
+    kind = {"A": "insert", "R": "remove"}
+    st = GpuRxStack(device=-1, max_socks=1024, ip4_log2=cfg["log4"], ip6_log2=cfg["log6"],
+                    intf_hwport=cfg["hwports"])
+    half = len(ops) // 2
+    rcs0 = []
+    if rank == 0:  # rank 0 owns the sockets and the first half of the ops
+        rcs0 = ts.replay(st, socks, ops, upto=half)
+    shards.broadcast_tables(st, torch, dist, "cpu", 0)
+    rcs = []
+    for at in range(half, len(ops), 500):  # the rest in batches, socket churn between
+        batch = [(kind[o[0]], o[2], o[1], o[3], o[4], o[5], o[6], o[7]) for o in ops[at:at + 500]]
+        s = socks[(at // 500) % len(socks)]
+        s.hwports ^= 1
+        batch.append(("sock", s.id, ts.sock_struct(s)))
+        rcs += shards.broadcast_ops(st, batch if rank == 0 else None, torch, dist, "cpu", 0)
+    img = torch.from_numpy(st.image_host())
+    ref = img.clone()
+    dist.broadcast(ref, src=0)
+    got_rcs = torch.tensor(rcs, dtype=torch.int64)
+    ref_rcs = got_rcs.clone()
+    dist.broadcast(ref_rcs, src=0)
+    same = torch.tensor([int(torch.equal(img, ref) and torch.equal(got_rcs, ref_rcs))])
+    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        q.put((int(same.item()), rcs0 + rcs, img.numpy().tobytes()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_incremental_table_ops_keep_ranks_identical():
+    """the replicated tables are kept current with incremental
+    updates -- after the image broadcast, op batches from rank 0 leave both
+    ranks' tables byte-identical, and equal to one stack that applied the
+    whole script itself (return codes included)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ops_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    same, rcs, img = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert same == 1
+    import table_scripts as ts
+    from onload_amd.rx import GpuRxStack
+    cfg, socks, ops = ts.build("mixed")
+    ops = [o for o in ops if o[0] in "AR"]
+    st = GpuRxStack(device=-1, max_socks=1024, ip4_log2=cfg["log4"], ip6_log2=cfg["log6"],
+                    intf_hwport=cfg["hwports"])
+    half = len(ops) // 2
+    want = ts.replay(st, socks, ops, upto=half)
+    for at in range(half, len(ops), 500):
+        want += ts.replay(st, [], ops[at:at + 500])
+        s = socks[(at // 500) % len(socks)]
+        s.hwports ^= 1
+        want.append(st.sock_set(s.id, ts.sock_struct(s)))
+    assert rcs == want
+    assert img == st.image_host().tobytes()
+    assert any(rc != 0 for rc in want)  # the script reaches -ENOBUFS / -ENOENT paths
 
 
 def test_shard_ranges_cover_exactly():
