@@ -15,7 +15,21 @@ SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_table_kernel.hip 
            onload_amd/csrc/oo_gpu_rx.cpp onload_amd/csrc/oo_rx_csum.cpp
 HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 
-all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling
+# Builds of the same kernels with other ring / extra-round / wave counts
+# (distinct sonames: loaded beside the product in one process).  The kernel's
+# static vmcnt waits are written in terms of these constants;
+# tests/test_gpu_wait_variants.py runs parity on every build.
+CHECK_VARIANTS := r6e4:-DOO_RX_RING=6,-DOO_RX_EXTRA=4 r8e2:-DOO_RX_RING=8,-DOO_RX_EXTRA=2 \
+                  w1e0:-DOO_RX_WAVES=1,-DOO_RX_EXTRA=0
+CHECKS := $(foreach v,$(CHECK_VARIANTS),build/check/liboo_gpu_rx_$(firstword $(subst :, ,$(v))).so)
+
+all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling $(CHECKS)
+
+build/check/liboo_gpu_rx_%.so: $(SRCS) $(HDRS)
+	@mkdir -p build/check
+	$(HIPCC) $(HIPFLAGS) -Wno-pass-failed $(subst $(COMMA), ,$(word 2,$(subst :, ,$(filter $*:%,$(CHECK_VARIANTS))))) \
+	  -shared -Wl,-soname,liboo_gpu_rx_$*.so -o $@ $(SRCS)
+COMMA := ,
 
 $(PRODUCT): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,liboo_gpu_rx.so -o $@ $(SRCS)

@@ -167,6 +167,13 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is part of the image
         pass
+    _lib = bind_library(path)
+    return _lib
+
+
+def bind_library(path: str) -> ctypes.CDLL:
+    """dlopen one build of the library and declare its C ABI (a build with
+    its own soname loads beside the product: tests/test_gpu_wait_variants.py)."""
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in ABI_SYMBOLS.items():
         fn = getattr(lib, name)
@@ -174,7 +181,6 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         fn.argtypes = args
     if lib.oo_gpu_rx_abi_version() != ABI_VERSION:
         raise RuntimeError("onload_amd: ABI version mismatch")
-    _lib = lib
     return lib
 
 

@@ -57,8 +57,8 @@ class GpuRxStack:
 
     def __init__(self, device: int = 0, max_socks: int = 8192, ip4_log2: int = 16,
                  ip6_log2: int = 14, intf_hwport=(0,), host_stage_bytes: int = 0,
-                 host_stage_pkts: int = 0):
-        self._lib = _abi.load_library()
+                 host_stage_pkts: int = 0, lib=None):
+        self._lib = lib if lib is not None else _abi.load_library()
         cfg = _abi.Cfg()
         cfg.device = device
         cfg.max_socks = max_socks
