@@ -1233,6 +1233,12 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
   const uint32_t nb = body_chunks(off0, span);
   const uint32_t rounds = (nb + 7u) >> 3;
   const uint64_t bm = __ballot(nb != 0);
+  if (bm == 0) {  // no frame reaches past its window (64-B frames): no jobs
+    myslot = lane;
+    Jobs J;
+    J.lo = J.hi = J.nb = J.lim = J.rj = J.T = 0;
+    return J;
+  }
   uint32_t myq;
   const uint32_t r0 = bm ? (uint32_t)__builtin_amdgcn_readlane((int)rounds, __builtin_ctzll(bm)) : 0u;
   if (__ballot(nb != 0 && rounds != r0) == 0) {  // all jobs alike: list order
@@ -1455,12 +1461,22 @@ __device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, ui
 __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64],
                                              uint32_t lane) {
   const uint32_t lo = (uint32_t)dv.abase, hi = (uint32_t)(dv.abase >> 32);
+  // Every row's frame fields first (24 permutes, one wait), then the eight
+  // DMAs: fetched row by row, each row waited for its own permutes.
+  uint32_t l[HC], h[HC], sp[HC];
+#pragma unroll
+  for (int i = 0; i < HC; ++i) {
+    const uint32_t p = (uint32_t)i * 8u + (lane >> 3);
+    l[i] = lane_get(lo, p);
+    h[i] = lane_get(hi, p);
+    sp[i] = lane_get((uint32_t)dv.span, p);
+  }
 #pragma unroll
   for (int i = 0; i < HC; ++i) {
     const uint32_t p = (uint32_t)i * 8u + (lane >> 3);
     const uint32_t c = ((lane & 7u) + p) & 7u;
-    const uint64_t ab = (uint64_t)lane_get(hi, p) << 32 | lane_get(lo, p);
-    const int nwin = ((int)lane_get((uint32_t)dv.span, p) + 15) >> 4;
+    const uint64_t ab = (uint64_t)h[i] << 32 | l[i];
+    const int nwin = ((int)sp[i] + 15) >> 4;
     glds<OO_RX_HDR_AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
   }
 }
@@ -1913,7 +1929,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     uint32_t T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
     if (lane == 0) lds_write4(&L.T0, T0);
     IssueCursor ci;
-    issue_slot(ci, J, 0, lane, zero);
+    if (T0 != 0) issue_slot(ci, J, 0, lane, zero);  // (body-less tiles issue no rounds)
     // This tile's header windows: older than the previous tile's NST stores
     // (none before the first tile) and the R rounds issued here.
     if (T != 0) {
@@ -2000,7 +2016,12 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // The consume side's cursor is set up only now: its registers are free
     // during the header work, where the demux loads need them.
     ConsumeCursor cc;
-    consume_start(cc, J, lane);
+    if (T0 != 0) {
+      consume_start(cc, J, lane);
+    } else {  // nothing to consume: every body sum is 0
+      cc.acc = 0;
+      cc.bs = 0;
+    }
 
     // ---- body stream, two pieces per step.  Each wait counts the
     // operations issued after the awaited pair (the demux loads excepted:
