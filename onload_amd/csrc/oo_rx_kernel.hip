@@ -2129,7 +2129,9 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void rx_kernel(KParams P) {
   tile_loop<false>(P);
 }
-__global__ __launch_bounds__(WAVES * 64) void tx_kernel(KParams P) { tile_loop<true>(P); }
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void tx_kernel(KParams P) {
+  tile_loop<true>(P);
+}
 
 }  // namespace oo_rx
 
