@@ -141,10 +141,20 @@ def run_rank(args) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N>1 path on a box with fewer GPUs than ranks (never
+    # for a measurement): OO_BENCH_SHARE_GPU=1 puts rank r on GPU r mod the
+    # GPUs present, OO_BENCH_BACKEND=gloo replaces RCCL (which takes one rank
+    # per GPU).
+    if os.environ.get("OO_BENCH_SHARE_GPU") == "1":
+        local %= max(1, torch.cuda.device_count())
+    backend = os.environ.get("OO_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     cfg = args.config
     n_per = args.n or DEFAULT_N[cfg]
