@@ -328,6 +328,19 @@ __device__ __forceinline__ void occ_words6(const Probe& t, const uint32_t i[6], 
       : "memory");
 }
 
+__device__ __forceinline__ void occ_words4(const Probe& t, const uint32_t i[4], uint32_t w[4]) {
+  uint64_t a[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a[k] = t.occ + 4u * (i[k] >> 5);
+  asm volatile(
+      "global_load_dword %0, %4, off\n\tglobal_load_dword %1, %5, off\n\t"
+      "global_load_dword %2, %6, off\n\tglobal_load_dword %3, %7, off\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+      : "memory");
+}
+
 __device__ __forceinline__ bool probe_occ(const KParams& P, const Probe& t, uint32_t i) {
   (void)P;
   return ((gload4(t.occ + 4u * (i >> 5)) >> (i & 31u)) & 1u) != 0;
@@ -1051,13 +1064,26 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
     const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
     const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
-    // All six bits in one batch (a UDP lane's stage-3 bits are unused).
+    // All the bits in one batch: six words, or four when no lane of the
+    // wave looks up TCP (UDP has no third stage).
     bool o0 = false, o1 = false, o2 = false, q0 = false, q1 = false, q2 = false;
+    const bool any_tcp = __ballot(look && tcp) != 0;
     if (look) {
       const uint32_t idx[6] = {h1_0, h1_1, h1_2, (h1_0 + h2_0) & t.mask, (h1_1 + h2_1) & t.mask,
                                (h1_2 + h2_2) & t.mask};
       uint32_t w[6];
-      occ_words6(t, idx, w);
+      if (any_tcp) {
+        occ_words6(t, idx, w);
+      } else {
+        const uint32_t i4[4] = {idx[0], idx[1], idx[3], idx[4]};
+        uint32_t w4[4];
+        occ_words4(t, i4, w4);
+        w[0] = w4[0];
+        w[1] = w4[1];
+        w[3] = w4[2];
+        w[4] = w4[3];
+        w[2] = w[5] = 0u;
+      }
       DSTAMP(8);
       auto bit = [&](int k) { return ((w[k] >> (idx[k] & 31u)) & 1u) != 0; };
       o0 = bit(0);
@@ -1079,7 +1105,7 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
       // Both families walk in one instruction stream (lookup_stages<2>).
       // Waves with TCP lookups (three stages, long connected-socket chains)
       // take the state machine; UDP-only waves the stage-by-stage walks.
-      if (OO_RX_FSM && __ballot(tcp) != 0)
+      if (OO_RX_FSM && any_tcp)
         m = lookup_fsm<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0, h1_1,
                                      h1_2, h2_0, h2_1, h2_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
       else
