@@ -170,6 +170,8 @@ struct oo_gpu_rx_ctx {
   bool dyn = true;             // dynamic tile claims (OO_RX_STATIC=1: static)
   uint32_t tail_tile = 32;     // packets per tile at the batch's end (dynamic)
   uint32_t tail_per_wave = 1;  // such tiles per wave
+  uint32_t ngroups_max = 0;    // claim groups at most (0: chosen per launch)
+  uint32_t gshift = ~0u;       // claim group of a wave: (gwave >> gshift) mod groups (~0u: per launch)
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t tstep = 8;          // tile size step (KParams::tstep)
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
@@ -645,6 +647,8 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   c->dyn = env_u32("OO_RX_STATIC", 0) == 0;
   c->tail_tile = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_TAIL_TILE", 32) / 8 * 8));
   c->tail_per_wave = env_u32("OO_RX_TAIL_PER_WAVE", 1);
+  c->ngroups_max = std::min<uint32_t>(CLAIM_GROUPS, env_u32("OO_RX_GROUPS", 0));  // 0: by frame size
+  c->gshift = env_u32("OO_RX_GSHIFT", ~0u);                                       // ~0: by frame size
   DevTables& T = c->T;
   T.ip4_mask = c->ip4_mask;
   T.ip6_mask = c->ip6_mask;
@@ -900,11 +904,18 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
   // The launch's claim counters (zero: every launch leaves them reset), one
-  // pair per wave group: the largest power of two <= CLAIM_GROUPS and <= W
-  // (every group has a wave).
+  // pair per wave group: the largest power of two <= the group limit with
+  // ngroups << gshift <= W (every group has a wave).  Short frames (under
+  // 1 KiB of buffer per packet: header-bound tiles, many claims per us) use
+  // 16 groups of eight-block runs, each group spread over all eight XCDs;
+  // long frames 64 groups of single waves (same-box A/B).
   P.claim = c->d_claim + 32u * CLAIM_GROUPS * (c->claim_seq++ % CLAIM_SLOTS);
+  const bool short_frames = P.frames_bytes < 1024ull * n;
+  uint32_t gmax = c->ngroups_max ? c->ngroups_max : (short_frames ? 16u : CLAIM_GROUPS);
+  P.gshift = std::min<uint32_t>(c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u), 16u);
+  while (P.gshift > 0 && (1ull << P.gshift) > W) --P.gshift;
   P.ngroups = 1;
-  while (P.ngroups < CLAIM_GROUPS && 2u * P.ngroups <= W) P.ngroups *= 2;
+  while (P.ngroups < gmax && (2ull * P.ngroups << P.gshift) <= W) P.ngroups *= 2;
   P.dyn = c->dyn ? 1u : 0u;
   if (c->dyn) {
     // Dynamic: full 64-packet tiles, then about tail_per_wave tiles of

@@ -164,7 +164,8 @@ struct KParams {
   uint8_t* sink;         // 64 x 32 B written by lanes without a packet (rx_kernel)
   uint64_t* stamps;      // diagnostic builds (OO_RX_STAMPS) only; may be null
   uint32_t* claim;       // per wave group, 128 B apart: {claims, finished waves}, 0 at launch
-  uint32_t ngroups;      // wave groups (a power of two dividing the wave count)
+  uint32_t ngroups;      // wave groups (a power of two, ngroups << gshift <= waves)
+  uint32_t gshift;       // wave gwave is in group (gwave >> gshift) mod ngroups
   uint32_t dyn;          // 1: tiles past a wave's first three are claimed
   uint8_t hwport[OO_GPU_RX_MAX_INTF];
 };

@@ -1888,6 +1888,19 @@ __device__ __forceinline__ void claim_tile(uint32_t* ctr, uint32_t step, uint32_
   if (lane == 0) got = __hip_atomic_fetch_add(ctr, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The claim group of wave gwave: runs of B = 2^gshift consecutive waves
+// (gshift 4: eight blocks, one on each XCD) dealt round-robin to the groups.
+__device__ __forceinline__ uint32_t group_of(const KParams& P, uint32_t gwave) {
+  return (gwave >> P.gshift) & (P.ngroups - 1u);
+}
+// The number of waves in group g of W (every group has one: ngroups << gshift
+// <= W): one run in every period of B ngroups waves, and part of the rest.
+__device__ __forceinline__ uint32_t group_members(const KParams& P, uint32_t g, uint32_t W) {
+  const uint32_t B = 1u << P.gshift, period = B * P.ngroups;
+  const uint32_t rem = W % period;
+  return W / period * B + (rem > g * B ? min(rem - g * B, B) : 0u);
+}
+
 // The per-wave tile loop of rx_kernel (TX = false) and tx_kernel (TX =
 // true): the same staging and body stream, different header work and stores.
 template <bool TX>
@@ -1910,8 +1923,9 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   // Group g's claims are g + 3 W, g + 3 W + ngroups, ... (its counter holds
   // the multiple of ngroups handed out); kept in LDS, out of the registers.
   if (lane == 0) {
-    lds_write4(&L.dbase, 3u * W + (gwave & (P.ngroups - 1u)));
-    lds_write4(&L.gofs, 32u * (gwave & (P.ngroups - 1u)));
+    const uint32_t g = group_of(P, gwave);
+    lds_write4(&L.dbase, 3u * W + g);
+    lds_write4(&L.gofs, 32u * g);
   }
   if (gwave < P.ntiles) {
   if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
@@ -2141,9 +2155,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   vm_wait<0>();
   if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
     uint32_t* const ctr = P.claim + lds_read4(&L.gofs);  // {claims, finished}
-    // the group's waves: gwave = g mod ngroups (ngroups <= W, a power of two)
-    const uint32_t g = lds_read4(&L.gofs) / 32u;
-    const uint32_t members = W / P.ngroups + (g < (W & (P.ngroups - 1u)) ? 1u : 0u);
+    const uint32_t members = group_members(P, lds_read4(&L.gofs) / 32u, W);
     const uint32_t done = atomicAdd(&ctr[1], 1u);
     if (done == members - 1u) {
       atomicExch(&ctr[0], 0u);
