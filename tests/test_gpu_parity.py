@@ -169,13 +169,37 @@ def test_full_size_config2_bit_exact(cuda):
     assert frac[_abi.R_DELIVER] > 0.98
 
 
-def test_full_size_config3_properties(cuda):
-    """BASELINE config 3 at 2^22 x 64 B (1/4 of full size) bit-exact."""
+def test_full_size_config3_bit_exact(cuda):
+    """BASELINE config 3 at full size: 2^24 x 64 B, every record."""
     filters, socks = pktgen.world(3)
     g, o = _pair(lambda s: s.load_world(filters, socks))
-    buf, desc = pktgen.generate(3, 1 << 22)
+    buf, desc = pktgen.generate(3, 1 << 24, nthreads=NTHREADS)
     got = _check(g, o, buf, desc)
     assert (got["stage"][got["reason"] == 0] == 2).all()
+
+
+def test_full_size_config4_bit_exact(cuda):
+    """BASELINE config 4 at the bench's full single-GPU size: 2^22 mixed
+    IPv4/TCP frames of 64-9014 B with IP and TCP options, every record."""
+    filters, socks = pktgen.world(4)
+    g, o = _pair(lambda s: s.load_world(filters, socks))
+    buf, desc = pktgen.generate(4, 1 << 22, nthreads=NTHREADS)
+    got = _check(g, o, buf, desc)
+    assert set(np.unique(got["stage"][got["reason"] == 0]).tolist()) == {1, 2, 3}
+
+
+def test_full_size_config5_last_shard_bit_exact(cuda):
+    """BASELINE config 5 at full per-GPU size: the 8th of the eight
+    byte-balanced shards of 2^27 IMIX TCP/UDP IPv4/IPv6 frames (what rank 7
+    processes in `bench.py --gpus 8`), every record."""
+    from onload_amd import shards
+    filters, socks = pktgen.world(5)
+    g, o = _pair(lambda s: s.load_world(filters, socks))
+    seed = pktgen.default_seed(5)
+    first, n = shards.shard_for(5, seed, 8 << 24, 7, 8)
+    buf, desc = pktgen.generate(5, n, seed=seed, first=first, nthreads=NTHREADS)
+    got = _check(g, o, buf, desc)
+    assert (got["reason"] == _abi.R_DELIVER).mean() > 0.9
 
 
 @pytest.mark.parametrize("env", [{"OO_RX_STATIC": "1"}, {"OO_RX_TAIL_TILE": "8", "OO_RX_TAIL_PER_WAVE": "3"},
