@@ -170,7 +170,6 @@ struct oo_gpu_rx_ctx {
   bool dyn = true;             // dynamic tile claims (OO_RX_STATIC=1: static)
   uint32_t tail_tile = 32;     // packets per tile at the batch's end (dynamic)
   uint32_t tail_per_wave = 1;  // such tiles per wave
-  uint32_t tail_mode = 0;      // 1: full tiles a multiple of the wave count
   uint32_t ngroups_max = 0;    // claim groups at most (0: chosen per launch)
   uint32_t gshift = ~0u;       // claim group of a wave: (gwave >> gshift) mod groups (~0u: per launch)
   uint32_t grid = 1024;        // resident blocks of rx_kernel
@@ -648,7 +647,6 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   c->dyn = env_u32("OO_RX_STATIC", 0) == 0;
   c->tail_tile = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_TAIL_TILE", 32) / 8 * 8));
   c->tail_per_wave = env_u32("OO_RX_TAIL_PER_WAVE", 1);
-  c->tail_mode = env_u32("OO_RX_TAIL_MODE", 0);
   c->ngroups_max = std::min<uint32_t>(CLAIM_GROUPS, env_u32("OO_RX_GROUPS", 0));  // 0: by frame size
   c->gshift = env_u32("OO_RX_GSHIFT", ~0u);                                       // ~0: by frame size
   DevTables& T = c->T;
@@ -926,10 +924,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
     // all end within a small tile of each other.
     const uint64_t S = c->tail_tile;
     const uint64_t tail = W * c->tail_per_wave * S;
-    uint64_t NA = n > tail ? (n - tail) / 64 : 0;
-    // tail_mode 1: the same number of full tiles for every wave (n / 64 W
-    // of them), the rest (under one full tile per wave) in small tiles.
-    if (c->tail_mode == 1) NA = (uint64_t)n / (64 * W) * W;
+    const uint64_t NA = n > tail ? (n - tail) / 64 : 0;
     const uint64_t NS = S < 64 ? (n - 64 * NA + S - 1) / S : 0;
     P.ntiles = (uint32_t)(NA + NS);
     P.tlo = (uint32_t)S;

@@ -206,8 +206,7 @@ def test_full_size_config5_last_shard_bit_exact(cuda):
                                  {"OO_RX_TAIL_TILE": "64"}, {"OO_RX_GRID_PCT": "37"},
                                  {"OO_RX_GSHIFT": "4", "OO_RX_GROUPS": "8"}, {"OO_RX_GSHIFT": "4"},
                                  {"OO_RX_GSHIFT": "5", "OO_RX_GROUPS": "16", "OO_RX_GRID_PCT": "37"},
-                                 {"OO_RX_GSHIFT": "0", "OO_RX_GROUPS": "64"}, {"OO_RX_TAIL_MODE": "1"},
-                                 {"OO_RX_TAIL_MODE": "1", "OO_RX_TAIL_TILE": "16"}])
+                                 {"OO_RX_GSHIFT": "0", "OO_RX_GROUPS": "64"}])
 def test_tile_partitions_and_claim_reuse(cuda, env, monkeypatch):
     """Static and dynamic (claimed) tile schedules with several tail shapes
     give the same records; 40 launches in a row reuse every claim-counter
