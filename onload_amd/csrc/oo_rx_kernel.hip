@@ -1729,7 +1729,9 @@ __device__ __forceinline__ void gstore2(uint64_t a, uint32_t v) {
   *reinterpret_cast<g_uint16*>(a) = (uint16_t)v;
 }
 constexpr int NST_TX = 6;
+#ifndef OO_RX_ABL_RX_ONLY  // timing builds of rx_kernel alone (tx_kernel then stores nothing)
 static_assert(R >= 4, "store_checks stages 64 lanes x 64 B in the ring");
+#endif
 __device__ __forceinline__ void store_checks(const KParams& P, const DescView& dv,
                                              const TxHdr& h, uint32_t l4v, uint32_t lane,
                                              uint4 (*ring)[64]) {
@@ -2124,7 +2126,11 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 
     const uint32_t body = lane_get(cc.bs, myslot);
     if constexpr (TX) {
+#ifndef OO_RX_ABL_RX_ONLY
       store_checks(P, dv, th, tx_l4_check(th, dv.shift, body), lane, L.ring);
+#else
+      (void)th;
+#endif
     } else {
       finish(ps, body);
       if (P.counters != nullptr && dv.valid)
