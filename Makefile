@@ -11,7 +11,7 @@ CFLAGS   ?= -O2 -std=gnu11 -fPIC -Wall -Wextra -Wno-unused-parameter
 PRODUCT := onload_amd/liboo_gpu_rx.so
 PKTGEN  := onload_amd/liboo_pktgen.so
 SHIM    := onload_amd/liboo_rx_poll.so
-SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_table_kernel.hip \
+SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_rx_kernel_short.hip onload_amd/csrc/oo_table_kernel.hip \
            onload_amd/csrc/oo_gpu_rx.cpp onload_amd/csrc/oo_rx_csum.cpp
 HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 

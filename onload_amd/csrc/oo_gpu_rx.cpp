@@ -32,6 +32,8 @@
 extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_tx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_rx_blocks_per_cu(void);
+extern "C" int oo_rx_launch_short(const oo_rx::KParams* P, int grid, hipStream_t stream);
+extern "C" int oo_rx_blocks_per_cu_short(void);
 extern "C" int oo_rx_waves_per_block(void);
 extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
                                    uint32_t n, uint32_t gen, hipStream_t s);
@@ -173,6 +175,8 @@ struct oo_gpu_rx_ctx {
   uint32_t ngroups_max = 0;    // claim groups at most (0: chosen per launch)
   uint32_t gshift = ~0u;       // claim group of a wave: (gwave >> gshift) mod groups (~0u: per launch)
   uint32_t grid = 1024;        // resident blocks of rx_kernel
+  uint32_t grid_short = 0;     // resident blocks of the short-frame rx_kernel (0: unused)
+  uint32_t kmode = 0;          // rx kernel: 0 by frame size, 1 always the 4-slot, 2 always the 2-slot
   uint32_t tstep = 8;          // tile size step (KParams::tstep)
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
   // host path
@@ -642,11 +646,15 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
     const int b0 = oo_rx_blocks_per_cu();
     if (b0 > 0)
       c->grid = std::max<uint32_t>(1, (uint32_t)(b0 * prop.multiProcessorCount) * pct / 100);
+    const int b1 = oo_rx_blocks_per_cu_short();
+    if (b1 > 0)
+      c->grid_short = std::max<uint32_t>(1, (uint32_t)(b1 * prop.multiProcessorCount) * pct / 100);
   }
   c->tstep = env_u32("OO_RX_TSTEP", 8) == 1 ? 1 : 8;
   c->dyn = env_u32("OO_RX_STATIC", 0) == 0;
   c->tail_tile = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_TAIL_TILE", 32) / 8 * 8));
   c->tail_per_wave = env_u32("OO_RX_TAIL_PER_WAVE", 1);
+  c->kmode = env_u32("OO_RX_KERNEL", 0);
   c->ngroups_max = std::min<uint32_t>(CLAIM_GROUPS, env_u32("OO_RX_GROUPS", 0));  // 0: by frame size
   c->gshift = env_u32("OO_RX_GSHIFT", ~0u);                                       // ~0: by frame size
   DevTables& T = c->T;
@@ -899,9 +907,17 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
   P.stamps = c->stamps;
   memcpy(P.hwport, c->hwport, sizeof(P.hwport));
+  // Short frames (under 1 KiB of buffer per packet) are bound by the per-tile
+  // header and table-lookup chain, not by the body stream: they take the
+  // 2-slot-ring rx_kernel, whose smaller LDS footprint fits 12 waves per CU
+  // instead of 10 (same-box A/B: config 3 -7 %, config 5 -2 %; config 2
+  // +11 %, so long frames keep the 4-slot ring).
+  const bool short_frames = P.frames_bytes < 1024ull * n;
+  const bool use_short = !tx && c->grid_short > 0 && (c->kmode == 2 || (c->kmode == 0 && short_frames));
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((need + wpb - 1) / wpb, c->grid));
+  const uint32_t blocks = std::max<uint32_t>(
+      1, std::min<uint32_t>((need + wpb - 1) / wpb, use_short ? c->grid_short : c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
   // The launch's claim counters (zero: every launch leaves them reset), one
   // pair per wave group: the largest power of two <= the group limit with
@@ -910,7 +926,6 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // 16 groups of eight-block runs, each group spread over all eight XCDs;
   // long frames 64 groups of single waves (same-box A/B).
   P.claim = c->d_claim + 32u * CLAIM_GROUPS * (c->claim_seq++ % CLAIM_SLOTS);
-  const bool short_frames = P.frames_bytes < 1024ull * n;
   uint32_t gmax = c->ngroups_max ? c->ngroups_max : (short_frames ? 16u : CLAIM_GROUPS);
   P.gshift = std::min<uint32_t>(c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u), 16u);
   while (P.gshift > 0 && (1ull << P.gshift) > W) --P.gshift;
@@ -953,7 +968,8 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
     P.tstep = (uint32_t)step;
   }
   const int grid = (int)blocks;
-  const int rc = tx ? oo_tx_launch(&P, grid, s) : oo_rx_launch(&P, grid, s);
+  const int rc = tx ? oo_tx_launch(&P, grid, s)
+                    : use_short ? oo_rx_launch_short(&P, grid, s) : oo_rx_launch(&P, grid, s);
   if (rc != 0) return -EIO;
   return note_launch(c, s);
 }

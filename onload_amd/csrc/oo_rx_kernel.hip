@@ -49,7 +49,15 @@
 
 #include "oo_rx_device.h"
 
+// OO_RX_SHORT (oo_rx_kernel_short.hip): the same rx_kernel with a 2-slot
+// ring, compiled into namespace oo_rx_short for short-frame batches (no
+// tx_kernel there: its check-field staging needs a 4-slot ring).
+#ifdef OO_RX_SHORT
+namespace oo_rx_short {
+using namespace ::oo_rx;
+#else
 namespace oo_rx {
+#endif
 
 typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1729,7 +1737,7 @@ __device__ __forceinline__ void gstore2(uint64_t a, uint32_t v) {
   *reinterpret_cast<g_uint16*>(a) = (uint16_t)v;
 }
 constexpr int NST_TX = 6;
-#ifndef OO_RX_ABL_RX_ONLY  // timing builds of rx_kernel alone (tx_kernel then stores nothing)
+#if !defined(OO_RX_ABL_RX_ONLY) && !defined(OO_RX_SHORT)  // (timing builds: rx_kernel alone)
 static_assert(R >= 4, "store_checks stages 64 lanes x 64 B in the ring");
 #endif
 __device__ __forceinline__ void store_checks(const KParams& P, const DescView& dv,
@@ -2173,12 +2181,29 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void rx_kernel(KParams P) {
   tile_loop<false>(P);
 }
+#ifndef OO_RX_SHORT
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void tx_kernel(KParams P) {
   tile_loop<true>(P);
 }
+#endif
 
 }  // namespace oo_rx
 
+#ifdef OO_RX_SHORT
+// Resident blocks per CU of the short-frame rx_kernel.
+extern "C" int oo_rx_blocks_per_cu_short(void) {
+  int b = 0;
+  const hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx_short::rx_kernel, oo_rx_short::WAVES * 64, 0);
+  return e == hipSuccess ? b : 0;
+}
+
+// Launch one RX batch of short frames on `stream`.
+extern "C" int oo_rx_launch_short(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx_short::rx_kernel, dim3(grid), dim3(oo_rx_short::WAVES * 64), 0, stream, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#else
 // Resident blocks per CU (sizes the persistent grid).
 extern "C" int oo_rx_blocks_per_cu(void) {
   int b = 0;
@@ -2201,3 +2226,4 @@ extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t strea
   hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif  // OO_RX_SHORT

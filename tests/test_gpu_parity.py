@@ -206,7 +206,8 @@ def test_full_size_config5_last_shard_bit_exact(cuda):
                                  {"OO_RX_TAIL_TILE": "64"}, {"OO_RX_GRID_PCT": "37"},
                                  {"OO_RX_GSHIFT": "4", "OO_RX_GROUPS": "8"}, {"OO_RX_GSHIFT": "4"},
                                  {"OO_RX_GSHIFT": "5", "OO_RX_GROUPS": "16", "OO_RX_GRID_PCT": "37"},
-                                 {"OO_RX_GSHIFT": "0", "OO_RX_GROUPS": "64"}])
+                                 {"OO_RX_GSHIFT": "0", "OO_RX_GROUPS": "64"}, {"OO_RX_KERNEL": "1"},
+                                 {"OO_RX_KERNEL": "2", "OO_RX_GRID_PCT": "37"}])
 def test_tile_partitions_and_claim_reuse(cuda, env, monkeypatch):
     """Static and dynamic (claimed) tile schedules with several tail shapes
     give the same records; 40 launches in a row reuse every claim-counter
@@ -227,3 +228,25 @@ def test_tile_partitions_and_claim_reuse(cuda, env, monkeypatch):
             assert got.tobytes() == want.tobytes(), (n, rep, diff_report(got, want, desc))
             np.testing.assert_array_equal(ctr, counters_of(want))
     g.close()
+
+
+@pytest.mark.parametrize("kernel", ["1", "2"])
+def test_both_rx_kernels_on_every_corpus(cuda, kernel, monkeypatch):
+    """The 4-slot-ring rx_kernel (long frames) and the 2-slot one (short
+    frames, 12 waves per CU) are chosen per launch by buffer bytes per packet
+    (oo_gpu_rx.cpp launch()); forced here (OO_RX_KERNEL 1 / 2), each must be
+    bit-exact on the edge corpus at odd and even alignments and on samples of
+    every configuration, with several launches per context."""
+    monkeypatch.setenv("OO_RX_KERNEL", kernel)
+    g, o = _pair(lambda s: install(s, edge_world()), intf_hwport=HWPORTS)
+    for shift in (0, 3):
+        buf, desc = pack(edge_frames(), align=64 if shift % 2 == 0 else 16, shift=shift)
+        _check(g, o, buf, desc)
+    g.close()
+    for config, n in ((2, 1 << 15), (3, 1 << 17), (4, 1 << 14), (5, 1 << 17)):
+        filters, socks = pktgen.world(config)
+        g, o = _pair(lambda s: s.load_world(filters, socks))
+        buf, desc = pktgen.generate(config, n, first=999 * config, nthreads=NTHREADS)
+        for _ in range(3):
+            _check(g, o, buf, desc)
+        g.close()

@@ -20,19 +20,31 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "onload_amd", "csrc", "oo_rx_kernel.hip")
+SRC_SHORT = os.path.join(ROOT, "onload_amd", "csrc", "oo_rx_kernel_short.hip")
+RX_SHORT = "_ZN11oo_rx_short9rx_kernelEN5oo_rx7KParamsE"
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
-@pytest.fixture(scope="module")
-def asm(tmp_path_factory):
+def _compile(tmp_path_factory, src):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     out = tmp_path_factory.mktemp("isa") / "k.s"
     r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950",
-                        "--offload-device-only", "-S", "-o", str(out), SRC,
+                        "--offload-device-only", "-S", "-o", str(out), src,
                         "-Rpass-analysis=kernel-resource-usage"],
                        capture_output=True, text=True, check=True)
     return out.read_text(), r.stderr
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    return _compile(tmp_path_factory, SRC)
+
+
+@pytest.fixture(scope="module")
+def asm_short(tmp_path_factory):
+    """The short-frame rx_kernel (2-slot ring, oo_rx_kernel_short.hip)."""
+    return _compile(tmp_path_factory, SRC_SHORT)
 
 
 def _body(text, name):
@@ -73,3 +85,15 @@ def test_store_counts(asm):
     assert not re.findall(r"global_store_(byte|dword\b|dwordx2)", tx)
     for body in (rx, tx):  # flat stores would count in lgkmcnt as well
         assert not re.findall(r"flat_store|flat_load|flat_atomic", body)
+
+
+def test_short_kernel_same_invariants(asm_short):
+    text, stderr = asm_short
+    u = _usage(stderr, RX_SHORT)
+    assert u["VGPRs Spill"] == 0, u
+    assert u["VGPRs"] <= 168, u
+    rx = _body(text, RX_SHORT)
+    assert "scratch_" not in rx
+    assert len(re.findall(r"global_store_dwordx4", rx)) == 2
+    assert not re.findall(r"global_store_(byte|short|dword\b|dwordx2)", rx)
+    assert not re.findall(r"flat_store|flat_load|flat_atomic", rx)
