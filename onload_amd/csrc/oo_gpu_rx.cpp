@@ -923,10 +923,10 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // pair per wave group: the largest power of two <= the group limit with
   // ngroups << gshift <= W (every group has a wave).  Short frames (under
   // 1 KiB of buffer per packet: header-bound tiles, many claims per us) use
-  // 16 groups of eight-block runs, each group spread over all eight XCDs;
+  // 32 groups of eight-block runs, each group spread over all eight XCDs;
   // long frames 64 groups of single waves (same-box A/B).
   P.claim = c->d_claim + 32u * CLAIM_GROUPS * (c->claim_seq++ % CLAIM_SLOTS);
-  uint32_t gmax = c->ngroups_max ? c->ngroups_max : (short_frames ? 16u : CLAIM_GROUPS);
+  uint32_t gmax = c->ngroups_max ? c->ngroups_max : (short_frames ? 32u : CLAIM_GROUPS);
   P.gshift = std::min<uint32_t>(c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u), 16u);
   while (P.gshift > 0 && (1ull << P.gshift) > W) --P.gshift;
   P.ngroups = 1;
