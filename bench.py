@@ -78,6 +78,9 @@ def parse_args(argv=None):
     ap.add_argument("--xdp-host", action="store_true",
                     help="also time zero-copy AF_XDP ingest: UMEM and ring in registered host "
                          "memory read by the kernel over PCIe")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="also time consecutive batches alternating over two streams (a side "
+                         "measurement: never value)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-memory path: oo_gpu_rx_submit/_wait, pinned "
                          "double-buffered H2D + transform + D2H")
@@ -269,6 +272,10 @@ def run_rank(args) -> None:
     if args.scatter and world > 1:
         extras["rccl_scatter"] = time_scatter(torch, dist, shards, cfg, seed, n_total, rank,
                                               world, dev, buf)
+    if args.pipelined:
+        extras["pipelined_2stream"] = time_pipelined(torch, stack, frames, d_desc, n, my_mean, out,
+                                                     dev, stream, args.steps, args.warmup)
+        log(f"[rank {rank}] pipelined: {json.dumps(extras['pipelined_2stream'])}")
     if args.host_path:
         extras["host_path"] = time_host_path(torch, filters, socks, buf, desc, local)
         log(f"[rank {rank}] host path: {json.dumps(extras['host_path'])}")
@@ -483,6 +490,40 @@ def time_xdp_host(torch, stack, buf, desc, ref_out, dev, sh, reps=5, headroom=19
             "pcie_GBps": round((frame_bytes + 16 * n) / (ms * 1e-3) / 1e9, 2),
             "umem_bytes": int(umem.nbytes), "headroom": headroom,
             "records_equal_descriptor_path": same}
+
+
+def time_pipelined(torch, stack, frames, d_desc, n, mean_len, out, dev, stream, steps, warmup):
+    """Consecutive batches alternating over two streams (each its own result
+    buffer): a batch's launch no longer waits for the previous one to drain,
+    so the next batch's blocks take the CUs as the previous batch's last
+    waves finish, and the launch gap overlaps. Region / K over both streams;
+    a side measurement (a kernel's own duration is no longer region / K)."""
+    s2 = torch.cuda.Stream(dev)
+    out2 = torch.empty_like(out)
+    streams = (stream, s2)
+    bufs = (out, out2)
+
+    def run(k):
+        for i in range(k):
+            st = streams[i & 1]
+            stack.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
+                                      bufs[i & 1].data_ptr(), 0, st.cuda_stream)
+
+    run(warmup)
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    s2.wait_event(ev0)
+    run(steps)
+    join = torch.cuda.Event()
+    join.record(s2)
+    stream.wait_event(join)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = float(ev0.elapsed_time(ev1)) / steps
+    gbs = (mean_len + DESC_B + RESULT_B) * n / (ms * 1e-3) / 1e9
+    return {"ms_per_batch": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 2),
+            "achieved_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "streams": 2}
 
 
 def time_host_path(torch, filters, socks, buf, desc, device, batch=1 << 16, reps=3):
