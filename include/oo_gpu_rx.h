@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OO_GPU_RX_ABI_VERSION 2
+#define OO_GPU_RX_ABI_VERSION 3
 
 /* intf_i -> hwport map size (CI_CFG_MAX_INTERFACES = 30,
  * src/include/ci/internal/transport_config_opt.h:29). */
@@ -88,6 +88,10 @@ enum {
                                   (doff 8, options NOP NOP TS 10: tcp_rx.c:4537-4543,
                                   CI_TCP_TSO_WORD ip_shared_types.h:2742); the host
                                   reads TSval/TSecr at l4_off + 24 / + 28         */
+#define OO_RX_F_UDP_S2  0x40u  /* UDP decided in stage 1 with one match, and the
+                                  stage-2 (laddr, lport) lookup matches too: the
+                                  union the future rule counts holds more than one
+                                  socket (udp_internal.h:41-52, :86-97)           */
 
 /* One frame in the batch.  16 bytes. */
 typedef struct oo_gpu_pkt_desc {
@@ -111,7 +115,8 @@ typedef struct oo_gpu_pkt_desc {
  *  - lookups ran (DELIVER or
  *    NO_MATCH):                   hash3 (stage-1 __onload_hash3, rxp.hash),
  *                                 flags&MCAST
- *  - DELIVER:                     sock, stage, nmatch, flags&MULTI
+ *  - DELIVER:                     sock, stage, nmatch, flags&MULTI,
+ *                                 flags&UDP_S2 (IPv4 UDP, stage 1, nmatch 1)
  * For IPv6, saddr/daddr hold onload_addr_xor() of the address (the value the
  * hash consumes, src/include/onload/hash.h:31-42); the full addresses are in
  * the frame at l4_off - 32 and l4_off - 16.
@@ -222,6 +227,13 @@ int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* ctx, int32_t sock_id,
                        const oo_gpu_rx_sock* sock);
 /* Apply pending table/socket changes to the device on `stream` now. */
 int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* ctx, void* stream);
+/* Streams.  The context remembers the streams it launched on (nothing is
+ * recorded per batch): a table change enqueues an event on each of them at
+ * that moment and waits for it, so every stream used with the context must
+ * stay valid until the context is closed -- or until this call, made before
+ * destroying it, which records the stream's last event and stops using the
+ * stream itself.  0 (also for a stream the context never used), -EIO. */
+int oo_gpu_rx_stream_done(oo_gpu_rx_ctx* ctx, void* stream);
 
 /* Table image: the context's whole table state (slot records with route
  * counts, tombstones and the socket fields they name; socket records) as one
@@ -330,6 +342,16 @@ int oo_gpu_rx_submit(oo_gpu_rx_ctx* ctx, const void* frames, uint64_t frames_byt
                      const oo_gpu_pkt_desc* desc, uint32_t n, oo_gpu_rx_result* out,
                      oo_gpu_rx_counters* delta, uint64_t* ticket);
 int oo_gpu_rx_wait(oo_gpu_rx_ctx* ctx, uint64_t ticket);
+
+/* Asynchronous zero-copy batch: frames, descriptors and results are device
+ * addresses -- HBM, or registered host memory (oo_gpu_rx_host_register's
+ * dev_ptr: a packet-buffer pool / UMEM read in place, over PCIe) -- and
+ * nothing is copied.  Runs on one of the two staging slots' streams like
+ * oo_gpu_rx_submit (the context needs host staging; its sizes do not bound
+ * this call) and completes with oo_gpu_rx_wait (returns n).  0 or -errno. */
+int oo_gpu_rx_submit_mapped(oo_gpu_rx_ctx* ctx, const void* d_frames, uint64_t frames_bytes,
+                            const oo_gpu_pkt_desc* d_desc, uint32_t n,
+                            oo_gpu_rx_result* d_out, uint64_t* ticket);
 
 /* submit + wait.  Returns n or -errno. */
 int oo_gpu_rx_batch(oo_gpu_rx_ctx* ctx, const void* frames,

@@ -21,9 +21,11 @@
  *       -> ops->pkt_handler                   handle_rx_pkt (:288-373: it
  *          passes the packet to the kernel and does its own counting)
  *   a resolved "future" socket: IPv4 TCP decided in lookup stage 1
- *   (ci_tcp_handle_rx_pre_future, tcp_rx.h:150-184), or IPv4 UDP unicast
- *   with one match in the deciding stage (ci_udp_rx_deliver_to_future,
- *   udp_internal.h:41-103)
+ *   (ci_tcp_handle_rx_pre_future, tcp_rx.h:150-184), or IPv4 UDP whose two
+ *   lookup stages together match exactly one socket
+ *   (ci_udp_rx_deliver_to_future, udp_internal.h:41-103: a second match in
+ *   either stage gives the future up; the record's nmatch and
+ *   OO_RX_F_UDP_S2 say so)
  *       -> ops->post_future                   ci_{tcp,udp}_handle_rx_post_future
  *          (tcp_rx.h:198-214, udp_internal.h:116-134) with future->socket set;
  *          a non-zero return means the socket cannot take it now (recvq
@@ -37,11 +39,25 @@
  *
  * and keeps the stack counters the replaced code keeps (struct
  * oo_rx_poll_stats: the stats_def.h / ip_stats_ops.h counters, by name).
- * Packets the transform does not take -- multi-buffer (scatter) RX events and
- * discard events outside the checksum class -- go to ops->other_ev unchanged.
+ * RX events the transform does not take -- multi-buffer (scatter) events,
+ * plain events when sw_verify is 0, frames not inside one buffer of the pool
+ * -- go to ops->other_ev unchanged, for the caller's existing per-event
+ * code, which also counts their rx_evs (netif_event.c:1718); discard events
+ * outside the checksum class are released (:1175-1183).
  *
  * All calls happen on the caller's thread, under the stack lock, before
- * oo_rx_poll_evs returns, in event order.
+ * oo_rx_poll_evs returns, in event order.  (An integration that queues
+ * other_ev events for its old loop, as integration/netif_event_gpu.c does,
+ * runs them after the batch's transformed packets: on AF_XDP, the
+ * north-star case, only non-whole-buffer events take that path, and AF_XDP
+ * delivers single-buffer frames, efxdp_vi.c:343-348.)
+ *
+ * The batch path: the events are taken evs_per_poll at a time, two device
+ * batches in flight (the next one's transform overlaps this one's
+ * dispatch).  With OO_RX_POLL_ZERO_COPY the packet-buffer pool is
+ * registered with the device at open and each frame is read where the NIC
+ * put it (over PCIe, no host copy); otherwise the frames of a batch are
+ * gathered into a registered buffer first.
  */
 #ifndef OO_RX_POLL_H
 #define OO_RX_POLL_H
@@ -104,7 +120,8 @@ typedef struct oo_rx_poll_future {
  * src/include/ci/internal/stats_def.h (netif stats) and ip_stats_ops.h
  * (ipv4 / ip6 / tcp / udp).  oo_rx_poll_evs adds to them. */
 typedef struct oo_rx_poll_stats {
-  uint64_t rx_evs;                  /* stats_def.h:57, netif_event.c:1718/:1189 */
+  uint64_t rx_evs;                  /* stats_def.h:57, netif_event.c:1718/:1189
+                                       (events handed to other_ev excluded)    */
   uint64_t rx_sw_csum_pass;         /* stats_def.h:881, netif_event.c:1190      */
   uint64_t rx_discard_csum_bad;     /* stats_def.h:521, netif_event.c:1170      */
   uint64_t rx_discard_len_err;      /* netif_event.c:1165                        */
@@ -157,8 +174,13 @@ typedef struct oo_rx_poll_cfg {
                                north-star case); 0: only discard events in the
                                checksum class do (:1155-1162), plain RX events
                                go to other_ev                                  */
-  uint32_t    rsvd;
+  uint32_t    flags;        /* OO_RX_POLL_ZERO_COPY, or 0                      */
 } oo_rx_poll_cfg;
+
+/* cfg.flags: register pkt_bufs with the device and read frames in place
+ * (falls back to gathering if the pool cannot be registered; see
+ * oo_rx_poll_zero_copy). */
+#define OO_RX_POLL_ZERO_COPY 0x1u
 
 typedef struct oo_rx_poll oo_rx_poll;
 
@@ -169,11 +191,17 @@ int  oo_rx_poll_open(oo_rx_poll** out, oo_gpu_rx_ctx* gpu, const oo_rx_poll_cfg*
 void oo_rx_poll_close(oo_rx_poll* p);
 
 /* Handle n events (any number: they are taken evs_per_poll at a time) and
- * add to *stats.  Returns n, or -errno if the device failed -- then no
- * callback has run for the events of the failed batch and later ones, and
- * the caller still owns them (the reference CPU path can take them). */
+ * add to *stats.  Returns n.  If the device fails, the call stops at the
+ * failed batch: no callback has run and no counter was added for its events
+ * and the later ones, which the caller still owns (the reference CPU path
+ * can take them); the return value is then the number of events handled
+ * before it (< n), or -errno if that is 0.  -EINVAL for bad arguments. */
 int  oo_rx_poll_evs(oo_rx_poll* p, const oo_rx_poll_ev* evs, uint32_t n,
                     oo_rx_poll_stats* stats);
+
+/* 1 if frames are read in place (OO_RX_POLL_ZERO_COPY took), 0 if they are
+ * gathered, -EINVAL. */
+int  oo_rx_poll_zero_copy(const oo_rx_poll* p);
 
 #ifdef __cplusplus
 }

@@ -29,8 +29,8 @@
 struct gpu_poll_ctx {
   ci_netif* ni;
   struct ci_netif_poll_state* ps;
-  ef_event* leftover;              /* events for the existing loop */
-  int n_leftover;
+  const oo_rx_poll_ev* evs;        /* the shim's events of this call       */
+  uint8_t* handback;               /* per shim event: other_ev gave it back */
 };
 
 static ci_ip_pkt_fmt* gpu_pkt(ci_netif* ni, uint32_t id)
@@ -125,12 +125,7 @@ static void gpu_release(void* arg, uint32_t id, const uint8_t* frame,
 static void gpu_other_ev(void* arg, const oo_rx_poll_ev* e)
 {
   struct gpu_poll_ctx* c = arg;
-  ef_event* ev = &c->leftover[c->n_leftover++];
-  ev->rx.type = EF_EVENT_TYPE_RX;
-  ev->rx.rq_id = e->rq_id;
-  ev->rx.ofs = e->ofs;
-  ev->rx.len = e->len;
-  ev->rx.flags = e->flags;
+  c->handback[e - c->evs] = 1;     /* the existing loop takes the original */
 }
 
 /* Discard subtypes as the shim's flags (the inverse of
@@ -212,28 +207,34 @@ int ci_netif_rx_gpu_open(ci_netif* ni, struct ci_netif_gpu_rx* g, int device,
 
 /* The batched RX branch, in place of the per-event RX cases of
  * ci_netif_poll_evq (netif_event.c:1715-1742, :1843): the RX / RX_DISCARD
- * events of one ef_eventq_poll (:1697) of interface intf_i go to the device
- * in one batch; other events, and whatever the shim hands back, are left in
- * leftover[] for the existing loop.  Returns how many. */
+ * events of one ef_eventq_poll (:1697, at most 16 events; EF_EVS_PER_POLL
+ * bounds a poll, opts_netif_def.h:976-984) of interface intf_i go to the
+ * device in one batch.  Other events, the events the shim hands back
+ * (other_ev) and -- if the device fails -- every RX event it did not get to,
+ * are copied to leftover[] in their original order for the existing loop.
+ * Returns how many. */
 int ci_netif_rx_batch_gpu(ci_netif* ni, struct ci_netif_poll_state* ps,
                           struct ci_netif_gpu_rx* g, ef_vi* evq, int intf_i,
                           const ef_event* ev, int n_evs, ef_event* leftover)
 {
-  oo_rx_poll_ev e[64];
+  enum { MAX_EVS = 64 };
+  oo_rx_poll_ev e[MAX_EVS];
+  int16_t shim_of[MAX_EVS];        /* original event -> shim index, or -1 */
+  uint8_t handback[MAX_EVS];
   oo_rx_poll_stats st;
-  int i, n = 0;
+  int i, n = 0, handled, n_left = 0;
+  if( n_evs > MAX_EVS )
+    n_evs = MAX_EVS;               /* the caller polls at most 16 at a time */
   memset(&st, 0, sizeof(st));
   memset(e, 0, sizeof(e));
+  memset(handback, 0, sizeof(handback));
   g->c.ps = ps;
-  g->c.leftover = leftover;
-  g->c.n_leftover = 0;
+  g->c.evs = e;
+  g->c.handback = handback;
   for( i = 0; i < n_evs; ++i ) {
     oo_pkt_p pp;
     ci_ip_pkt_fmt* pkt;
-    if( n == (int)(sizeof(e) / sizeof(e[0])) ) {
-      leftover[g->c.n_leftover++] = ev[i];
-      continue;
-    }
+    shim_of[i] = -1;
     if( EF_EVENT_TYPE(ev[i]) == EF_EVENT_TYPE_RX ) {
       OO_PP_INIT(ni, pp, EF_EVENT_RX_RQ_ID(ev[i]));
       pkt = PKT_CHK(ni, pp);
@@ -253,21 +254,23 @@ int ci_netif_rx_batch_gpu(ci_netif* ni, struct ci_netif_poll_state* ps,
       e[n].discard = gpu_discard_flags(EF_EVENT_RX_DISCARD_TYPE(ev[i]));
     }
     else {
-      leftover[g->c.n_leftover++] = ev[i];
       continue;
     }
     e[n].ofs = (uint16_t)(pkt->pkt_start_off + CI_MEMBER_OFFSET(ci_ip_pkt_fmt, dma_start));
     e[n].intf_i = (int16_t) intf_i;
     e[n].rsvd = 0;
     pkt->pay_len = e[n].len;
-    ++n;
+    shim_of[i] = (int16_t) n++;
   }
-  if( oo_rx_poll_evs(g->poll, e, (uint32_t) n, &st) < 0 ) {
-    /* Device lost: no callback ran; the CPU loop takes every event. */
-    for( i = 0; i < n_evs; ++i )
-      leftover[i] = ev[i];
-    return n_evs;
-  }
+  /* n, or fewer if the device failed part-way: events from `handled` on ran
+   * no callback and added no counter (oo_rx_poll.h) -- the CPU loop takes
+   * them, so nothing is released or delivered twice. */
+  handled = oo_rx_poll_evs(g->poll, e, (uint32_t) n, &st);
+  if( handled < 0 )
+    handled = 0;
   gpu_add_stats(ni, &st);
-  return g->c.n_leftover;
+  for( i = 0; i < n_evs; ++i )
+    if( shim_of[i] < 0 || shim_of[i] >= handled || handback[shim_of[i]] )
+      leftover[n_left++] = ev[i];
+  return n_left;
 }

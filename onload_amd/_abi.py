@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboo_gpu_rx.so")
 PKTGEN_PATH = os.path.join(_HERE, "liboo_pktgen.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_INTF = 32
 
 # Reason codes (oo_gpu_rx.h), in the reference's check order.
@@ -31,6 +31,7 @@ REASON_NAMES = {
 }
 
 F_IP6, F_VLAN, F_CSUM_OK, F_MCAST, F_MULTI, F_TSO = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
+F_UDP_S2 = 0x40
 SOCK_CONNECTED, SOCK_BIND2DEV = 0x1, 0x2
 
 DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("len", "<u2"), ("intf_i", "<i2"),
@@ -122,6 +123,7 @@ ABI_SYMBOLS = {
                                             ctypes.POINTER(_I32), ctypes.POINTER(_U16)]),
     "oo_gpu_rx_sock_set": (ctypes.c_int, [_P, _I32, ctypes.POINTER(Sock)]),
     "oo_gpu_rx_sync_tables": (ctypes.c_int, [_P, _P]),
+    "oo_gpu_rx_stream_done": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_process_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _P]),
     "oo_gpu_tx_fill_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P]),
     "oo_gpu_rx_xdp_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _U32, _U32, ctypes.c_int,
@@ -131,6 +133,7 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_batch": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P]),
     "oo_gpu_rx_submit": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, ctypes.POINTER(_U64)]),
     "oo_gpu_rx_wait": (ctypes.c_int, [_P, _U64]),
+    "oo_gpu_rx_submit_mapped": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, ctypes.POINTER(_U64)]),
     "oo_gpu_rx_host_register": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_P)]),
     "oo_gpu_rx_host_unregister": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_table_image_bytes": (_U64, [_P]),

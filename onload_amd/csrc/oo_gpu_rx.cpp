@@ -95,16 +95,25 @@ static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
               "entry layouts");
 
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
-constexpr int NTRACK = 8;             // streams whose last launch is tracked
+constexpr int NTRACK = 8;             // streams tracked at once (LRU)
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
-constexpr uint32_t CLAIM_SLOTS = 16;  // tile-claim counter sets (launches in flight)
+constexpr uint32_t CLAIM_SLOTS = NTRACK;  // tile-claim counter sets: one per tracked stream
 constexpr uint32_t CLAIM_GROUPS = 64; // wave groups per launch at most (128 B each)
 
-// The last launch on one stream (cross-stream ordering of table changes).
+// One stream the context launches on.  Nothing is recorded per launch: a
+// table change (flush_ops) records `ev` on every other stream that launched
+// since the last change and makes its own stream wait for it, which orders
+// the change after every batch already enqueued there.  The entry's index
+// is also the stream's tile-claim counter set: launches on one stream run in
+// order, so the set is free whenever the stream's next launch starts; an
+// entry handed to another stream makes that stream wait for the old one
+// first (track_of).
 struct Tracked {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
-  bool live = false;      // ev recorded since the last table flush waited on it
+  bool used = false;      // assigned to s
+  bool live = false;      // launched on s since a table change last ordered itself after s
+  bool gone = false;      // oo_gpu_rx_stream_done: ev already covers all of s's work
   uint32_t tables_seen = 0;  // table generation this stream has waited for
   uint64_t lru = 0;
 };
@@ -168,7 +177,7 @@ struct oo_gpu_rx_ctx {
   uint64_t lru = 0;
   uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros + the sink
   uint32_t* d_claim = nullptr; // CLAIM_SLOTS x CLAIM_GROUPS counter pairs, 128 B apart
-  uint32_t claim_seq = 0;      // launches so far (picks the pair)
+  bool failed = false;         // a table flush failed part-way: the device copy is unknown
   bool dyn = true;             // dynamic tile claims (OO_RX_STATIC=1: static)
   uint32_t tail_tile = 32;     // packets per tile at the batch's end (dynamic)
   uint32_t tail_per_wave = 1;  // such tiles per wave
@@ -482,91 +491,133 @@ void free_dev(oo_gpu_rx_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
-// The tracked entry of stream s (least recently used one reassigned; a
-// reassigned entry whose launch may still run is waited for first).
-Tracked& track_of(oo_gpu_rx_ctx* c, hipStream_t s) {
+// An event that completes once everything enqueued on t's stream so far
+// has: recorded now (a stream given up with oo_gpu_rx_stream_done already
+// has its final one).
+hipEvent_t mark(Tracked& t) {
+  if (!t.gone && hipEventRecord(t.ev, t.s) != hipSuccess) return nullptr;
+  return t.ev;
+}
+
+// The tracked entry of stream s (the least recently used one reassigned).
+// Reassigning an entry makes s wait for everything enqueued on its old
+// stream: that frees the entry's claim counters for s, and s carries the
+// old stream's table reads (live) into the next table change.  Returns
+// nullptr on a HIP failure.
+Tracked* track_of(oo_gpu_rx_ctx* c, hipStream_t s) {
   Tracked* victim = &c->track[0];
   for (Tracked& t : c->track) {
-    if (t.ev != nullptr && t.s == s) {
+    if (t.used && !t.gone && t.s == s) {
       t.lru = ++c->lru;
-      return t;
+      return &t;
     }
-    if (t.ev == nullptr) {
+    if (!t.used) {
       victim = &t;
       break;
     }
     if (t.lru < victim->lru) victim = &t;
   }
+  bool live = false;
   if (victim->ev == nullptr) {
-    (void)hipEventCreateWithFlags(&victim->ev, hipEventDisableTiming);
-  } else if (victim->live) {
-    (void)hipEventSynchronize(victim->ev);
+    if (hipEventCreateWithFlags(&victim->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+  } else if (victim->used) {
+    hipEvent_t e = mark(*victim);
+    if (e == nullptr || hipStreamWaitEvent(s, e, 0) != hipSuccess) return nullptr;
+    live = victim->live;
   }
   victim->s = s;
-  victim->live = false;
+  victim->used = true;
+  victim->gone = false;
+  victim->live = live;
   victim->tables_seen = 0;
   victim->lru = ++c->lru;
-  return *victim;
+  return victim;
 }
 
-// Pending table ops -> device, on stream s: first wait for every launch on
-// another stream that may still read the tables (no batch sees a
-// half-updated table), then copy the ops through a pinned staging buffer and
-// apply them (table_ops), then refresh the socket fields of the slots whose
-// socket changed.  No host synchronisation unless a staging buffer is still
-// in use by an earlier flush that has not run.
-int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
-  if (c->ops.empty()) return 0;
+uint32_t track_index(const oo_gpu_rx_ctx* c, const Tracked* t) { return (uint32_t)(t - c->track); }
+
+// Stream s follows every batch enqueued on another stream that may still
+// read the tables (no batch sees a half-updated table).
+int order_after_batches(oo_gpu_rx_ctx* c, hipStream_t s) {
   for (Tracked& t : c->track) {
-    if (t.ev != nullptr && t.live && t.s != s) {
-      if (hipStreamWaitEvent(s, t.ev, 0) != hipSuccess) return -EIO;
+    if (t.used && t.live && (t.gone || t.s != s)) {
+      hipEvent_t e = mark(t);
+      if (e == nullptr || hipStreamWaitEvent(s, e, 0) != hipSuccess) return -EIO;
       t.live = false;
     }
   }
+  return 0;
+}
+
+// Pending table ops -> device, on stream s: first order s after the
+// batches on other streams, then copy the ops through a pinned staging
+// buffer and apply them (table_ops), then refresh the socket fields of the
+// slots whose socket changed.  No host synchronisation unless a staging
+// buffer is still in use by an earlier flush that has not run.  A failure
+// after the first chunk has been enqueued leaves the device tables in an
+// unknown state: the context then refuses every later call (-EIO) rather
+// than apply the queued ops twice.
+int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
+  if (c->ops.empty()) return 0;
+  if (order_after_batches(c, s) != 0) return -EIO;
   const uint32_t total = (uint32_t)c->ops.size();
   for (uint32_t at = 0; at < total; at += OPS_CHUNK) {
     const uint32_t n = std::min(OPS_CHUNK, total - at);
     OpStage& st = c->stage[c->stage_next];
     c->stage_next ^= 1;
-    if (st.pending && hipEventSynchronize(st.ev) != hipSuccess) return -EIO;
+    if (st.pending && hipEventSynchronize(st.ev) != hipSuccess) {
+      c->failed = at > 0;
+      return -EIO;
+    }
     memcpy(st.h, c->ops.data() + at, sizeof(TableOp) * n);
     if (hipMemcpyAsync(st.d, st.h, sizeof(TableOp) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
         oo_table_launch_ops(&c->T, st.d, n, c->gen, s) != 0 ||
-        hipEventRecord(st.ev, s) != hipSuccess)
+        hipEventRecord(st.ev, s) != hipSuccess) {
+      c->failed = true;  // this chunk or an earlier one may have reached the device
       return -EIO;
+    }
     st.pending = true;
   }
-  if (c->ops_sock && oo_table_launch_refresh(&c->T, c->gen, s) != 0) return -EIO;
+  if (c->ops_sock && oo_table_launch_refresh(&c->T, c->gen, s) != 0) {
+    c->failed = true;
+    return -EIO;
+  }
   c->ops.clear();
   c->ops_sock = false;
   ++c->gen;
   ++c->tables_gen;
-  if (hipEventRecord(c->tables_ev, s) != hipSuccess) return -EIO;
+  Tracked* t = track_of(c, s);
+  if (t == nullptr || hipEventRecord(c->tables_ev, s) != hipSuccess) {
+    c->failed = true;
+    return -EIO;
+  }
   c->tables_stream = s;
-  track_of(c, s).tables_seen = c->tables_gen;
+  t->tables_seen = c->tables_gen;
   return 0;
 }
 
 // Everything a launch on stream s must follow: pending table ops, or the
-// last flush when it ran on another stream.
-int prepare(oo_gpu_rx_ctx* c, hipStream_t s) {
-  if (!c->ops.empty()) return flush_ops(c, s);
-  if (c->tables_gen == 0) return 0;
-  Tracked& t = track_of(c, s);
-  if (t.tables_seen != c->tables_gen) {
+// last flush when it ran on another stream.  Returns s's tracked entry.
+int prepare(oo_gpu_rx_ctx* c, hipStream_t s, Tracked** out = nullptr) {
+  if (c->failed) return -EIO;
+  if (!c->ops.empty()) {
+    const int rc = flush_ops(c, s);
+    if (rc) return rc;
+  }
+  Tracked* t = track_of(c, s);
+  if (t == nullptr) return -EIO;
+  if (c->tables_gen != 0 && t->tables_seen != c->tables_gen) {
     if (c->tables_stream != s && hipStreamWaitEvent(s, c->tables_ev, 0) != hipSuccess)
       return -EIO;
-    t.tables_seen = c->tables_gen;
+    t->tables_seen = c->tables_gen;
   }
+  if (out) *out = t;
   return 0;
 }
 
-int note_launch(oo_gpu_rx_ctx* c, hipStream_t s) {
-  Tracked& t = track_of(c, s);
-  if (hipEventRecord(t.ev, s) != hipSuccess) return -EIO;
-  t.live = true;
-  return 0;
-}
+// A launch (or copy) on s that reads the tables: the next table change
+// orders itself after it.
+void note_launch(Tracked* t) { t->live = true; }
 
 bool in_reg(const oo_gpu_rx_ctx* c, const void* p, uint64_t bytes) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -789,6 +840,19 @@ int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   return prepare(c, static_cast<hipStream_t>(stream));
 }
 
+int oo_gpu_rx_stream_done(oo_gpu_rx_ctx* c, void* stream) {
+  if (c == nullptr) return -EINVAL;
+  if (!has_dev(c)) return 0;
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (Tracked& t : c->track) {
+    if (!t.used || t.gone || t.s != s) continue;
+    if (hipEventRecord(t.ev, s) != hipSuccess) return -EIO;
+    t.gone = true;  // ev now covers all of s's work; s is never touched again
+  }
+  return 0;
+}
+
 uint64_t oo_gpu_rx_table_image_bytes(const oo_gpu_rx_ctx* c) {
   return c == nullptr ? 0 : image_hdr(c).total;
 }
@@ -803,7 +867,8 @@ int oo_gpu_rx_table_export(oo_gpu_rx_ctx* c, void* dst, uint64_t bytes, void* st
   }
   if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  int rc = prepare(c, s);
+  Tracked* t = nullptr;
+  int rc = prepare(c, s, &t);
   if (rc) return rc;
   uint8_t* d = static_cast<uint8_t*>(dst);
   const uint64_t n4 = c->ip4_mask + 1ull, n6 = c->ip6_mask + 1ull;
@@ -820,7 +885,8 @@ int oo_gpu_rx_table_export(oo_gpu_rx_ctx* c, void* dst, uint64_t bytes, void* st
       hipMemcpyAsync(d + h.off_socks, c->T.socks, sizeof(oo_gpu_rx_sock) * c->max_socks,
                      hipMemcpyDefault, s) == hipSuccess;
   if (!ok) return -EIO;
-  return note_launch(c, s);  // the copies read the tables like a batch
+  note_launch(t);  // the copies read the tables like a batch
+  return 0;
 }
 
 int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, void* stream) {
@@ -846,9 +912,7 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, vo
   // the device arrays are copied on the stream after every earlier use.
   c->ops.clear();
   c->ops_sock = false;
-  for (Tracked& t : c->track)
-    if (t.ev != nullptr && t.live && t.s != s && hipStreamWaitEvent(s, t.ev, 0) != hipSuccess)
-      return -EIO;
+  if (order_after_batches(c, s) != 0) return -EIO;
   if (hipMemcpyAsync(host.data(), src, h.total, hipMemcpyDefault, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return -EIO;
@@ -867,11 +931,21 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, vo
       hipMemcpyAsync(c->T.socks, d + h.off_socks, sizeof(oo_gpu_rx_sock) * c->max_socks,
                      hipMemcpyDefault, s) == hipSuccess &&
       oo_table_launch_occ(&c->T, s) == 0;
-  if (!ok) return -EIO;
+  // From here on the mirror holds the image: a failure leaves the device
+  // copy unknown.
+  Tracked* t = ok ? track_of(c, s) : nullptr;
+  if (t == nullptr) {
+    c->failed = true;
+    return -EIO;
+  }
   ++c->tables_gen;
-  if (hipEventRecord(c->tables_ev, s) != hipSuccess) return -EIO;
+  if (hipEventRecord(c->tables_ev, s) != hipSuccess) {
+    c->failed = true;
+    return -EIO;
+  }
   c->tables_stream = s;
-  track_of(c, s).tables_seen = c->tables_gen;
+  t->tables_seen = c->tables_gen;
+  c->failed = false;  // the whole table state was replaced on both sides
   return 0;
 }
 
@@ -925,7 +999,11 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // 1 KiB of buffer per packet: header-bound tiles, many claims per us) use
   // 32 groups of eight-block runs, each group spread over all eight XCDs;
   // long frames 64 groups of single waves (same-box A/B).
-  P.claim = c->d_claim + 32u * CLAIM_GROUPS * (c->claim_seq++ % CLAIM_SLOTS);
+  // The stream's own claim counter set (Tracked): launches on one stream
+  // run in order, and every launch leaves its counters reset.
+  Tracked* trk = track_of(c, s);
+  if (trk == nullptr) return -EIO;
+  P.claim = c->d_claim + 32u * CLAIM_GROUPS * track_index(c, trk);
   uint32_t gmax = c->ngroups_max ? c->ngroups_max : (short_frames ? 32u : CLAIM_GROUPS);
   P.gshift = std::min<uint32_t>(c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u), 16u);
   while (P.gshift > 0 && (1ull << P.gshift) > W) --P.gshift;
@@ -971,7 +1049,8 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   const int rc = tx ? oo_tx_launch(&P, grid, s)
                     : use_short ? oo_rx_launch_short(&P, grid, s) : oo_rx_launch(&P, grid, s);
   if (rc != 0) return -EIO;
-  return note_launch(c, s);
+  if (!tx) note_launch(trk);
+  return 0;
 }
 
 int oo_gpu_rx_process_dev(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
@@ -1069,8 +1148,11 @@ int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
     // No batch may still read it.
     for (HostSlot& s : c->slot)
       if (s.busy) (void)hipEventSynchronize(s.done);
-    for (Tracked& t : c->track)
-      if (t.ev != nullptr && t.live) (void)hipEventSynchronize(t.ev);
+    for (Tracked& t : c->track) {
+      if (!t.used) continue;
+      hipEvent_t e = mark(t);
+      if (e != nullptr) (void)hipEventSynchronize(e);
+    }
     (void)hipHostUnregister(p);
     c->regs.erase(c->regs.begin() + (long)i);
     return 0;
@@ -1142,6 +1224,39 @@ int oo_gpu_rx_submit(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes
   s.n = n;
   s.out = out;
   s.delta = delta;
+  c->next_ticket = t + 1;
+  *ticket = t;
+  return 0;
+}
+
+int oo_gpu_rx_submit_mapped(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
+                            const oo_gpu_pkt_desc* d_desc, uint32_t n, oo_gpu_rx_result* d_out,
+                            uint64_t* ticket) {
+  if (c == nullptr || ticket == nullptr ||
+      (n > 0 && (d_frames == nullptr || d_desc == nullptr || d_out == nullptr)))
+    return -EINVAL;
+  if (!has_dev(c)) return -ENODEV;
+  if (c->stage_pkts == 0) return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+  const uint64_t t = c->next_ticket;
+  HostSlot& s = c->slot[t % NSLOT];
+  if (s.busy) {
+    const int rc = complete_slot(c, s);
+    if (rc < 0) return rc;
+  }
+  hipStream_t st = s.stream;
+  if (n > 0) {
+    int rc = prepare(c, st);
+    if (rc == 0) rc = launch(c, d_frames, frames_bytes, d_desc, n, d_out, nullptr, st);
+    if (rc) return rc;
+  }
+  if (hipEventRecord(s.done, st) != hipSuccess) return -EIO;
+  s.busy = true;
+  s.ticket = t;
+  s.n = n;
+  s.out = d_out;
+  s.delta = nullptr;
+  s.copy_out = false;
   c->next_ticket = t + 1;
   *ticket = t;
   return 0;

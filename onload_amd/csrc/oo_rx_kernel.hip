@@ -922,7 +922,8 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
                                                uint32_t proto, int intf_i, int vlan, bool tcp,
                                                uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
                                                bool o0, bool o1, bool o2, bool q0, bool q1,
-                                               bool q2, Rec rec, int fs, int& stage) {
+                                               bool q2, Rec rec, int fs, int& stage,
+                                               bool& s2) {
   const uint32_t zero[4] = {0, 0, 0, 0};
   const bool six = M == 1 || (M == 2 && t.is6);
   const uint32_t dx = six ? (h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3]) : h.da[0];
@@ -938,10 +939,21 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
                       hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0, tcp);
   DSTAMP(11);
   stage = 1;
-  if (m.n == 0) {
-    m = walk<M>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
-                  hash2(dx, dport, 0u, 0u, proto), o1, rec1, fs == 1 || pre1, q1, tcp);
-    stage = 2;
+  // Stage 2 for the lanes stage 1 left undecided and, for the future rule's
+  // union (udp_internal.h:41-52, :86-97), for IPv4 UDP lanes with one
+  // stage-1 match: there only whether it matches at all (OO_RX_F_UDP_S2).
+  const bool probe = !tcp && !six && m.n == 1;
+  s2 = false;
+  if (m.n == 0 || probe) {
+    const Match m2 = walk<M>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
+                             hash2(dx, dport, 0u, 0u, proto), o1, rec1, fs == 1 || pre1, q1,
+                             tcp || probe);
+    if (probe) {
+      s2 = m2.n != 0;
+    } else {
+      m = m2;
+      stage = 2;
+    }
   }
   DSTAMP(12);
   if (m.n == 0 && tcp) {
@@ -970,10 +982,16 @@ __device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bo
                                             uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
                                             uint32_t h2_0, uint32_t h2_1, uint32_t h2_2, bool o0,
                                             bool o1, bool o2, bool q0, bool q1, bool q2, Rec rec,
-                                            int fs, int& stage) {
+                                            int fs, int& stage, bool& s2) {
   const uint32_t nst = tcp ? 3u : 2u;  // o2 (and q2) are false for UDP
+  const bool six = M == 1 || (M == 2 && t.is6);
   (void)o0;
   Match m = {-1, 0};
+  // probe: an IPv4 UDP lane decided in stage 1 with one match walks stage 2
+  // for the future rule's union (udp_internal.h:41-52, :86-97): s2 = it
+  // matches too.
+  bool probe = false;
+  s2 = false;
   uint32_t s = (uint32_t)fs;  // the first stage whose first slot is occupied (3: none)
   bool live = s < nst;
   uint32_t h1 = s == 0 ? h1_0 : s == 1 ? h1_1 : h1_2;
@@ -997,9 +1015,14 @@ __device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bo
         int32_t id;
         if (rec_match_m<M>(P, t, rec, k == 0, la, dport, ra, !st0, st0 ? sport : 0u, proto,
                            intf_i, vlan, id)) {
-          if (m.n == 0) m.first = id;
-          ++m.n;
-          end = tcp;  // TCP's deliver callbacks end the walk at the first match
+          if (probe) {
+            s2 = true;
+            end = true;
+          } else {
+            if (m.n == 0) m.first = id;
+            ++m.n;
+            end = tcp;  // TCP's deliver callbacks end the walk at the first match
+          }
         }
         if (!end) {
           h1 = (h1 + h2) & t.mask;
@@ -1010,9 +1033,20 @@ __device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bo
         }
       }
       if (end) {
-        if (m.n != 0) {
-          live = false;  // this stage decides
-          stage = (int)s + 1;
+        if (probe) {
+          live = false;
+        } else if (m.n != 0) {
+          stage = (int)s + 1;  // this stage decides
+          live = false;
+          if (!tcp && !six && s == 0 && m.n == 1 && o1) {
+            probe = true;  // and stage 2 is walked for the future rule
+            live = true;
+            s = 1;
+            h1 = h1_1;
+            first = h1;
+            h2 = h2_1;
+            k = 0;
+          }
         } else {
           // on to the next stage whose first slot is occupied
           ++s;
@@ -1062,6 +1096,7 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
   const uint32_t dx = is6 ? h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3] : h.da[0];
   Match m = {-1, 0};
   int stage = 0;
+  bool s2 = false;
   if (__ballot(look) != 0) {
     constexpr bool any6 = ANY6;
     const Probe t = probe_of(P, ANY6 && is6);
@@ -1115,10 +1150,12 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
       // take the state machine; UDP-only waves the stage-by-stage walks.
       if (OO_RX_FSM && any_tcp)
         m = lookup_fsm<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0, h1_1,
-                                     h1_2, h2_0, h2_1, h2_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
+                                     h1_2, h2_0, h2_1, h2_2, o0, o1, o2, q0, q1, q2, rec, fs, stage,
+                                     s2);
       else
         m = lookup_stages<ANY6 ? 2 : 0, !ANY6>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp,
-                                               h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage);
+                                               h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage,
+                                               s2);
       DSTAMP(10);
     }
   }
@@ -1155,6 +1192,7 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
       r.sock = m.first;
       r.nmatch = (uint16_t)m.n;
       if (m.n > 1) flags |= OO_RX_F_MULTI;
+      if (s2) flags |= OO_RX_F_UDP_S2;
     }
   }
   r.reason = (uint8_t)reason;
@@ -1885,7 +1923,11 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
       const uint32_t a = lane_get(w[d], q), b = lane_get(w[4 + d], q);
       vw[d] = hi ? b : a;
     }
+#ifdef OO_RX_ABL_HOTSTORE  // ablation builds only: every tile's records to one of 32 hot 2-KiB runs
+    out[(size_t)((t.key & 31u) * 64u + q) * 2u + hi] = v;
+#else
     out[(size_t)(t.first + q) * 2u + hi] = v;
+#endif
   }
 }
 

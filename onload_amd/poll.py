@@ -73,7 +73,10 @@ class Ops(ctypes.Structure):
 class PollCfg(ctypes.Structure):
     _fields_ = [("pkt_bufs", ctypes.c_void_p), ("pkt_bufs_bytes", ctypes.c_uint64),
                 ("buf_size", ctypes.c_uint32), ("evs_per_poll", ctypes.c_uint32),
-                ("sw_verify", ctypes.c_uint32), ("rsvd", ctypes.c_uint32)]
+                ("sw_verify", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+ZERO_COPY = 0x1  # OO_RX_POLL_ZERO_COPY
 
 
 POLL_SYMBOLS = {
@@ -82,6 +85,7 @@ POLL_SYMBOLS = {
     "oo_rx_poll_close": (None, [ctypes.c_void_p]),
     "oo_rx_poll_evs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.POINTER(Stats)]),
+    "oo_rx_poll_zero_copy": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 _lib = None
@@ -118,7 +122,7 @@ class RxPoll:
     alive by this object)."""
 
     def __init__(self, stack, pool: np.ndarray, buf_size: int, evs_per_poll: int,
-                 sw_verify: bool, handlers):
+                 sw_verify: bool, handlers, zero_copy: bool = False):
         self._lib = load_poll()
         self.pool = pool
         self.h = handlers
@@ -132,7 +136,8 @@ class RxPoll:
                        OTHER_EV(lambda a, e: h.other_ev(
                            np.frombuffer(ctypes.string_at(e, 16), EV_DTYPE)[0])),
                        None)
-        cfg = PollCfg(pool.ctypes.data, pool.nbytes, buf_size, evs_per_poll, int(sw_verify), 0)
+        cfg = PollCfg(pool.ctypes.data, pool.nbytes, buf_size, evs_per_poll, int(sw_verify),
+                      ZERO_COPY if zero_copy else 0)
         p = ctypes.c_void_p()
         rc = self._lib.oo_rx_poll_open(ctypes.byref(p), stack._ctx, ctypes.byref(cfg),
                                        ctypes.byref(self._cb))
@@ -145,6 +150,11 @@ class RxPoll:
         evs = np.ascontiguousarray(evs, dtype=EV_DTYPE)
         return self._lib.oo_rx_poll_evs(self._p, evs.ctypes.data, len(evs),
                                         ctypes.byref(self.stats))
+
+    @property
+    def zero_copy(self) -> bool:
+        """Frames are read in place (the pool is registered with the device)."""
+        return self._lib.oo_rx_poll_zero_copy(self._p) == 1
 
     def close(self) -> None:
         if self._p:

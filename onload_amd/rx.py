@@ -165,6 +165,12 @@ class GpuRxStack:
         if rc:
             raise OSError(-rc, "oo_gpu_rx_sync_tables")
 
+    def stream_done(self, stream: int) -> None:
+        """The caller is about to destroy `stream` (oo_gpu_rx_stream_done)."""
+        rc = self._lib.oo_gpu_rx_stream_done(self._ctx, ctypes.c_void_p(stream))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_stream_done")
+
     # -- the transform --------------------------------------------------
     def handle_rx_batch_dev(self, frames_ptr: int, frames_bytes: int, desc_ptr: int, n: int,
                             out_ptr: int, counters_ptr: int = 0, stream: int = 0) -> None:

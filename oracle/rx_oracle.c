@@ -658,6 +658,17 @@ static match_t walk6(const oo_or_tables* t, const uint8_t* la, uint32_t lp,
   return m;
 }
 
+/* One IPv4 lookup stage from outside (tests/poll_util.py restates the
+ * future rule of udp_internal.h:41-103 over the stages' match counts). */
+int oo_or_walk4(const oo_or_tables* t, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
+                uint32_t proto, int intf_i, int vlan, int stop, int32_t* first)
+{
+  match_t m = walk4(t, la, lp, ra, rp, proto, intf_i, vlan, stop);
+  if( first )
+    *first = m.first;
+  return m.n;
+}
+
 /* ------------------------------------------------------------------ */
 /* IP options walk: ci_ip_options_parse (netif_event.c:135-185).  Option
  * lengths are read through plain (signed on x86) char, so a length byte
@@ -879,6 +890,11 @@ void oo_or_rx_one(const oo_or_tables* t, const uint8_t* frame, int len,
         r->nmatch = (uint16_t)m[s].n;
         if( m[s].n > 1 )
           r->flags |= OO_RX_F_MULTI;
+        /* The future rule's union (udp_internal.h:41-52, :86-97): after a
+         * single stage-1 match ci_udp_handle_rx_pre_future still walks
+         * stage 2, and any match there gives the future up. */
+        if( proto == 17 && !is6 && s == 0 && m[0].n == 1 && m[1].n > 0 )
+          r->flags |= OO_RX_F_UDP_S2;
         break;
       }
   }

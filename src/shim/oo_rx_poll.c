@@ -4,15 +4,18 @@
  * liboo_gpu_rx.  See include/oo_rx_poll.h for the contract; each step below
  * names the reference code whose behaviour it keeps.
  *
- * One call of oo_rx_poll_evs:
- *   1. classify each event (netif_event.c:1715-1742 RX branch, :1843
- *      discard_rx_multi_pkts): transform / release / other_ev, and count the
- *      per-event stats the loop keeps (rx_evs, rx_discard_*);
- *   2. pack the frames to transform into one registered host buffer at 64-B
- *      alignment and run oo_gpu_rx_batch over them (one device batch per
- *      evs_per_poll events);
- *   3. walk the records in event order and dispatch each one through the
- *      callback table, counting what the replaced code counts.
+ * One call of oo_rx_poll_evs takes its events evs_per_poll at a time
+ * ("chunks"), two chunks in flight:
+ *   1. classify each event of a chunk (netif_event.c:1715-1742 RX branch,
+ *      :1843 discard_rx_multi_pkts): transform / release / other_ev, and
+ *      count the per-event stats the loop keeps (rx_evs, rx_discard_*);
+ *   2. describe the frames to transform -- in place in the packet-buffer
+ *      pool when it is registered with the device (zero copy: the kernel
+ *      reads them over PCIe), else gathered into a registered buffer -- and
+ *      submit the chunk's device batch;
+ *   3. while the next chunk's batch runs, wait for this one and walk its
+ *      records in event order, dispatching each through the callback table
+ *      and counting what the replaced code counts.
  */
 #include "oo_rx_poll.h"
 
@@ -20,20 +23,35 @@
 #include <stdlib.h>
 #include <string.h>
 
+enum { W_TRANSFORM = 0, W_RELEASE = 1, W_OTHER = 2 };
+
+/* One chunk's buffers; two of them alternate. */
+struct chunk {
+  oo_gpu_pkt_desc*  desc;      /* evs_per_poll descriptors (registered)     */
+  oo_gpu_rx_result* rec;       /* evs_per_poll records (registered)         */
+  void*             d_desc;    /* their device addresses (mapped)           */
+  void*             d_rec;
+  uint8_t*          pack;      /* gathered frames (gather mode, registered) */
+  void*             d_pack;
+  uint32_t*         ev_of;     /* transform slot -> event index             */
+  uint8_t*          what;      /* per event: W_*                            */
+  const oo_rx_poll_ev* evs;
+  uint32_t          n, m;      /* events, frames to transform               */
+  int               busy;      /* a device batch was submitted              */
+  uint64_t          ticket;
+  oo_rx_poll_stats  st;        /* the chunk's counters (land with it)       */
+};
+
 struct oo_rx_poll {
   oo_gpu_rx_ctx*   gpu;
   oo_rx_poll_cfg   cfg;
   oo_rx_poll_ops   ops;
-  uint8_t*         pack;       /* packed frames of one batch (registered) */
   uint64_t         pack_bytes;
-  oo_gpu_pkt_desc* desc;       /* evs_per_poll descriptors (registered)   */
-  oo_gpu_rx_result* rec;       /* evs_per_poll records (registered)       */
-  uint32_t*        ev_of;      /* batch slot -> event index               */
-  uint8_t*         what;       /* per event of the batch: enum step       */
-  int              registered; /* pack/desc/rec registered with the ctx   */
+  int              mapped;     /* chunk buffers registered: submit_mapped    */
+  int              zero_copy;  /* the pool is registered: frames in place    */
+  void*            d_pool;     /* its device address                         */
+  struct chunk     ch[2];
 };
-
-enum { W_TRANSFORM = 0, W_RELEASE = 1, W_OTHER = 2 };
 
 static uint64_t up64(uint64_t x) { return (x + 63u) & ~(uint64_t)63u; }
 
@@ -53,21 +71,54 @@ static void* alloc64(uint64_t bytes)
   return p;
 }
 
+/* Registers p with the device; 1 and *d set on success. */
+static int reg(oo_gpu_rx_ctx* gpu, void* p, uint64_t bytes, void** d)
+{
+  return oo_gpu_rx_host_register(gpu, p, bytes, d) == 0;
+}
+
+static void chunk_free(oo_rx_poll* p, struct chunk* c)
+{
+  if( c->d_desc )
+    oo_gpu_rx_host_unregister(p->gpu, c->desc);
+  if( c->d_rec )
+    oo_gpu_rx_host_unregister(p->gpu, c->rec);
+  if( c->d_pack )
+    oo_gpu_rx_host_unregister(p->gpu, c->pack);
+  free(c->pack);
+  free(c->desc);
+  free(c->rec);
+  free(c->ev_of);
+  free(c->what);
+}
+
 void oo_rx_poll_close(oo_rx_poll* p)
 {
+  int i;
   if( p == NULL )
     return;
-  if( p->registered ) {
-    oo_gpu_rx_host_unregister(p->gpu, p->pack);
-    oo_gpu_rx_host_unregister(p->gpu, p->desc);
-    oo_gpu_rx_host_unregister(p->gpu, p->rec);
+  for( i = 0; i < 2; ++i ) {
+    if( p->ch[i].busy )
+      (void)oo_gpu_rx_wait(p->gpu, p->ch[i].ticket);
+    chunk_free(p, &p->ch[i]);
   }
-  free(p->pack);
-  free(p->desc);
-  free(p->rec);
-  free(p->ev_of);
-  free(p->what);
+  if( p->d_pool )
+    oo_gpu_rx_host_unregister(p->gpu, (void*)p->cfg.pkt_bufs);
   free(p);
+}
+
+static int chunk_alloc(oo_rx_poll* p, struct chunk* c)
+{
+  const uint32_t n = p->cfg.evs_per_poll;
+  c->desc = alloc64(sizeof(oo_gpu_pkt_desc) * (uint64_t)n);
+  c->rec = alloc64(sizeof(oo_gpu_rx_result) * (uint64_t)n);
+  c->ev_of = malloc(sizeof(uint32_t) * (uint64_t)n);
+  c->what = malloc(n);
+  if( !p->zero_copy )
+    c->pack = alloc64(p->pack_bytes);
+  if( !c->desc || !c->rec || !c->ev_of || !c->what || (!p->zero_copy && !c->pack) )
+    return -ENOMEM;
+  return 0;
 }
 
 int oo_rx_poll_open(oo_rx_poll** out, oo_gpu_rx_ctx* gpu, const oo_rx_poll_cfg* cfg,
@@ -75,13 +126,15 @@ int oo_rx_poll_open(oo_rx_poll** out, oo_gpu_rx_ctx* gpu, const oo_rx_poll_cfg* 
 {
   oo_rx_poll* p;
   uint32_t n;
+  int i;
   if( out == NULL || gpu == NULL || cfg == NULL || ops == NULL )
     return -EINVAL;
   *out = NULL;
   n = cfg->evs_per_poll;
   if( n == 0 || n > OO_RX_POLL_MAX_EVS || cfg->buf_size == 0 ||
       (cfg->buf_size & (cfg->buf_size - 1)) != 0 || cfg->buf_size > 65536 ||
-      (cfg->pkt_bufs == NULL && cfg->pkt_bufs_bytes != 0) )
+      (cfg->pkt_bufs == NULL && cfg->pkt_bufs_bytes != 0) ||
+      (cfg->flags & ~(uint32_t)OO_RX_POLL_ZERO_COPY) != 0 )
     return -EINVAL;
   if( ops->post_future == NULL || ops->full_handler == NULL ||
       ops->pkt_handler == NULL || ops->release == NULL || ops->other_ev == NULL )
@@ -92,56 +145,71 @@ int oo_rx_poll_open(oo_rx_poll** out, oo_gpu_rx_ctx* gpu, const oo_rx_poll_cfg* 
   p->gpu = gpu;
   p->cfg = *cfg;
   p->ops = *ops;
-  /* A frame never exceeds the 16-bit event length; within a buffer it
-   * never exceeds buf_size. */
+  /* Zero copy: the kernel reads each frame where the NIC put it.  If the
+   * pool cannot be registered the shim gathers instead. */
+  if( (cfg->flags & OO_RX_POLL_ZERO_COPY) && cfg->pkt_bufs_bytes > 0 &&
+      reg(gpu, (void*)cfg->pkt_bufs, cfg->pkt_bufs_bytes, &p->d_pool) )
+    p->zero_copy = 1;
+  /* A transformed frame lies inside its buffer (frame_of): a gather buffer
+   * of evs_per_poll 64-B-aligned buffers holds any chunk. */
   p->pack_bytes = (uint64_t)n * up64(cfg->buf_size);
-  p->pack = alloc64(p->pack_bytes);
-  p->desc = alloc64(sizeof(oo_gpu_pkt_desc) * (uint64_t)n);
-  p->rec = alloc64(sizeof(oo_gpu_rx_result) * (uint64_t)n);
-  p->ev_of = malloc(sizeof(uint32_t) * (uint64_t)n);
-  p->what = malloc(n);
-  if( !p->pack || !p->desc || !p->rec || !p->ev_of || !p->what ) {
-    oo_rx_poll_close(p);
-    return -ENOMEM;
-  }
-  /* Registered staging: the H2D / D2H copies run straight from these
-   * buffers (no second memcpy through the context's pinned slots). */
-  if( oo_gpu_rx_host_register(gpu, p->pack, p->pack_bytes, NULL) == 0 ) {
-    if( oo_gpu_rx_host_register(gpu, p->desc, sizeof(oo_gpu_pkt_desc) * (uint64_t)n,
-                                NULL) == 0 ) {
-      if( oo_gpu_rx_host_register(gpu, p->rec, sizeof(oo_gpu_rx_result) * (uint64_t)n,
-                                  NULL) == 0 )
-        p->registered = 1;
-      else
-        oo_gpu_rx_host_unregister(gpu, p->desc);
+  p->mapped = 1;
+  for( i = 0; i < 2; ++i ) {
+    struct chunk* c = &p->ch[i];
+    if( chunk_alloc(p, c) != 0 ) {
+      oo_rx_poll_close(p);
+      return -ENOMEM;
     }
-    if( !p->registered )
-      oo_gpu_rx_host_unregister(gpu, p->pack);
+    /* Registered chunk buffers: the batch reads descriptors (and gathered
+     * frames) and writes records in place, nothing is staged. */
+    if( !reg(gpu, c->desc, sizeof(oo_gpu_pkt_desc) * (uint64_t)n, &c->d_desc) ||
+        !reg(gpu, c->rec, sizeof(oo_gpu_rx_result) * (uint64_t)n, &c->d_rec) ||
+        (!p->zero_copy && !reg(gpu, c->pack, p->pack_bytes, &c->d_pack)) )
+      p->mapped = 0;
+  }
+  if( !p->mapped && p->zero_copy ) {
+    /* Frames in place need mapped descriptors and records. */
+    oo_gpu_rx_host_unregister(gpu, (void*)cfg->pkt_bufs);
+    p->d_pool = NULL;
+    p->zero_copy = 0;
+    for( i = 0; i < 2; ++i )
+      if( (p->ch[i].pack = alloc64(p->pack_bytes)) == NULL ) {
+        oo_rx_poll_close(p);
+        return -ENOMEM;
+      }
   }
   *out = p;
   return 0;
 }
 
-/* The frame of an event inside the pool, or NULL if it does not lie inside
- * it (such an event is not the shim's to take). */
+int oo_rx_poll_zero_copy(const oo_rx_poll* p)
+{
+  return p == NULL ? -EINVAL : p->zero_copy;
+}
+
+/* The frame of an event, or NULL if it does not lie inside its buffer of the
+ * pool (such an event is not the shim's to take: ADVICE r2, a frame running
+ * past its buffer would overrun a gather slot). */
 static const uint8_t* frame_of(const oo_rx_poll* p, const oo_rx_poll_ev* e)
 {
   uint64_t off = (uint64_t)e->rq_id * p->cfg.buf_size + e->ofs;
-  if( e->ofs >= p->cfg.buf_size || off > p->cfg.pkt_bufs_bytes ||
+  if( (uint32_t)e->ofs + e->len > p->cfg.buf_size || off > p->cfg.pkt_bufs_bytes ||
       e->len > p->cfg.pkt_bufs_bytes - off )
     return NULL;
   return (const uint8_t*)p->cfg.pkt_bufs + off;
 }
 
 /* Step 1: what the poll loop does with an event before any transform
- * (netif_event.c:1715-1742 plain RX, :1131-1191 discard). */
+ * (netif_event.c:1715-1742 plain RX, :1131-1191 discard).  A plain RX event
+ * the shim does not take goes back to the caller's loop, which counts its
+ * rx_evs (:1718) itself. */
 static int classify(const oo_rx_poll* p, const oo_rx_poll_ev* e, oo_rx_poll_stats* st)
 {
   const int whole = (e->flags & (OO_RX_EV_SOP | OO_RX_EV_CONT)) == OO_RX_EV_SOP;
   if( e->discard == 0 ) {
-    ++st->rx_evs;                                          /* :1718 */
     if( !p->cfg.sw_verify || !whole || frame_of(p, e) == NULL )
       return W_OTHER;                                      /* reference branch */
+    ++st->rx_evs;                                          /* :1718 */
     return W_TRANSFORM;
   }
   /* discard_rx_multi_pkts: the class counter (:1164-1172) ... */
@@ -181,6 +249,24 @@ static void count_drop(const oo_gpu_rx_result* r, oo_rx_poll_stats* st)
   }
 }
 
+/* Whether the record resolves a future socket: IPv4 TCP decided in lookup
+ * stage 1 (ci_tcp_handle_rx_pre_future: the full 4-tuple lookup only,
+ * tcp_rx.h:150-184), or IPv4 UDP whose two lookup stages together hold
+ * exactly one socket (ci_udp_handle_rx_pre_future, udp_internal.h:58-103:
+ * ci_udp_rx_deliver_to_future keeps walking after the first match and gives
+ * up on a second one, :41-52; stage 2 runs whenever stage 1 did not give up,
+ * :93-97).  The device record carries the deciding stage's count (nmatch)
+ * and, for a stage-1 single match, whether stage 2 matches too
+ * (OO_RX_F_UDP_S2). */
+static int resolves_future(const oo_gpu_rx_result* r)
+{
+  if( (r->flags & OO_RX_F_IP6) || r->reason != OO_RX_R_DELIVER )
+    return 0;
+  if( r->proto == 6 )
+    return r->stage == 1;
+  return r->proto == 17 && r->nmatch == 1 && !(r->flags & OO_RX_F_UDP_S2);
+}
+
 /* Step 3 for a handled record (handle_rx_csum_bad returned 1):
  * __handle_rx_pkt -> handle_rx_pkt (:250-451) up to the transport call, then
  * the future seam. */
@@ -205,12 +291,7 @@ static void dispatch(oo_rx_poll* p, uint32_t id, const uint8_t* frame,
     ++st->in_recvs;                                        /* :282 */
     if( r->l4_off > pre_l3 + 20u )
       ++st->ip_options;                                    /* :181 */
-    /* The future seam (see oo_rx_poll.h): TCP decided in stage 1, or UDP
-     * unicast with a single match in its deciding stage. */
-    if( r->reason == OO_RX_R_DELIVER )
-      future = r->proto == 6 ? r->stage == 1
-             : r->proto == 17 && !(r->flags & (OO_RX_F_MCAST | OO_RX_F_MULTI)) &&
-               r->nmatch == 1;
+    future = resolves_future(r);
   }
   if( future ) {
     oo_rx_poll_future f;
@@ -252,83 +333,152 @@ static void dispatch(oo_rx_poll* p, uint32_t id, const uint8_t* frame,
     ++st->in_delivers;                                     /* :327 / :332 */
 }
 
-static int run_batch(oo_rx_poll* p, const oo_rx_poll_ev* evs, uint32_t n,
-                     oo_rx_poll_stats* st)
+/* Steps 1-2 for the chunk evs[0..n): classify, describe, submit.  0 or
+ * -errno (the chunk is then not in flight and nothing was counted). */
+static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs, uint32_t n,
+                        const oo_rx_poll_stats* base)
 {
   uint32_t i, m = 0;
   uint64_t at = 0;
-  oo_rx_poll_stats local;
   int rc;
-  /* Counters land only if the batch does: on a device failure the caller
-   * still owns every event from this batch on. */
-  local = *st;
+  c->evs = evs;
+  c->n = n;
+  c->busy = 0;
+  c->st = *base;
   for( i = 0; i < n; ++i ) {
     const oo_rx_poll_ev* e = &evs[i];
-    p->what[i] = (uint8_t)classify(p, e, &local);
-    if( p->what[i] == W_TRANSFORM ) {
-      oo_gpu_pkt_desc* d = &p->desc[m];
-      memcpy(p->pack + at, frame_of(p, e), e->len);
-      d->frame_off = at;
+    c->what[i] = (uint8_t)classify(p, e, &c->st);
+    if( c->what[i] == W_TRANSFORM ) {
+      oo_gpu_pkt_desc* d = &c->desc[m];
+      if( p->zero_copy ) {
+        d->frame_off = (uint64_t)e->rq_id * p->cfg.buf_size + e->ofs;
+      }
+      else {
+        /* frame_of bounds the frame by its buffer, and the gather buffer
+         * holds evs_per_poll 64-B-aligned buffers */
+        if( at + e->len > p->pack_bytes )
+          return -EINVAL;
+        memcpy(c->pack + at, frame_of(p, e), e->len);
+        d->frame_off = at;
+        at += up64(e->len);
+      }
       d->len = e->len;
       d->intf_i = e->intf_i;
       d->rsvd = 0;
-      p->ev_of[m++] = i;
-      at += up64(e->len);
+      c->ev_of[m++] = i;
     }
   }
-  if( m > 0 ) {
-    rc = oo_gpu_rx_batch(p->gpu, p->pack, at, p->desc, m, p->rec, NULL);
+  c->m = m;
+  if( m == 0 )
+    return 0;
+  if( p->zero_copy )
+    rc = oo_gpu_rx_submit_mapped(p->gpu, p->d_pool, p->cfg.pkt_bufs_bytes, c->d_desc, m,
+                                 c->d_rec, &c->ticket);
+  else if( p->mapped )
+    rc = oo_gpu_rx_submit_mapped(p->gpu, c->d_pack, at, c->d_desc, m, c->d_rec, &c->ticket);
+  else
+    rc = oo_gpu_rx_submit(p->gpu, c->pack, at, c->desc, m, c->rec, NULL, &c->ticket);
+  if( rc < 0 )
+    return rc;
+  c->busy = 1;
+  ++c->st.n_batches;
+  return 0;
+}
+
+/* Step 3: wait for the chunk's batch, then dispatch every event in order.
+ * The chunk's counters are added to *st only if its batch ran. */
+static int chunk_complete(oo_rx_poll* p, struct chunk* c, oo_rx_poll_stats* st)
+{
+  uint32_t i, m = 0;
+  if( c->busy ) {
+    int rc = oo_gpu_rx_wait(p->gpu, c->ticket);
+    c->busy = 0;
     if( rc < 0 )
       return rc;
-    ++local.n_batches;
   }
-  /* Step 3, in event order. */
-  m = 0;
-  for( i = 0; i < n; ++i ) {
-    const oo_rx_poll_ev* e = &evs[i];
-    if( p->what[i] == W_OTHER ) {
-      ++local.n_other;
+  for( i = 0; i < c->n; ++i ) {
+    const oo_rx_poll_ev* e = &c->evs[i];
+    if( c->what[i] == W_OTHER ) {
+      ++c->st.n_other;
       p->ops.other_ev(p->ops.arg, e);
     }
-    else if( p->what[i] == W_RELEASE ) {
-      ++local.n_release;
+    else if( c->what[i] == W_RELEASE ) {
+      ++c->st.n_release;
       p->ops.release(p->ops.arg, e->rq_id, frame_of(p, e), NULL);
     }
     else {
-      const oo_gpu_rx_result* r = &p->rec[m++];
+      const oo_gpu_rx_result* r = &c->rec[m++];
       const uint8_t* frame = frame_of(p, e);
       if( r->reason >= OO_RX_R_DROP_BASE ) {
-        count_drop(r, &local);
-        ++local.n_release;
+        count_drop(r, &c->st);
+        ++c->st.n_release;
         p->ops.release(p->ops.arg, e->rq_id, frame, r);
       }
       else {
         if( e->discard ) {         /* the discard path's double count, :1189-1190 */
-          ++local.rx_evs;
-          ++local.rx_sw_csum_pass;
+          ++c->st.rx_evs;
+          ++c->st.rx_sw_csum_pass;
         }
-        dispatch(p, e->rq_id, frame, r, &local);
+        dispatch(p, e->rq_id, frame, r, &c->st);
       }
     }
   }
-  *st = local;
+  *st = c->st;
   return 0;
 }
 
 int oo_rx_poll_evs(oo_rx_poll* p, const oo_rx_poll_ev* evs, uint32_t n,
                    oo_rx_poll_stats* stats)
 {
-  uint32_t done = 0;
+  uint32_t done = 0, issued, k;
+  int cur = 0, rc;
   if( p == NULL || stats == NULL || (n > 0 && evs == NULL) )
     return -EINVAL;
   if( n > (uint32_t)0x7fffffff )
     return -EINVAL;
-  while( done < n ) {
-    uint32_t k = n - done < p->cfg.evs_per_poll ? n - done : p->cfg.evs_per_poll;
-    int rc = run_batch(p, evs + done, k, stats);
-    if( rc < 0 )
-      return rc;
-    done += k;
+  if( n == 0 )
+    return 0;
+  /* Chunk i+1 is submitted before chunk i is waited for, so its transform
+   * overlaps chunk i's dispatch.  Each chunk's counters start from the
+   * counters with every earlier chunk in (it completes after them). */
+  k = n < p->cfg.evs_per_poll ? n : p->cfg.evs_per_poll;
+  if( (rc = chunk_submit(p, &p->ch[0], evs, k, stats)) < 0 )
+    return rc;
+  issued = k;
+  for( ;; ) {
+    struct chunk* c = &p->ch[cur];
+    struct chunk* nx = &p->ch[cur ^ 1];
+    int sub_rc = 0, more = issued < n;
+    oo_rx_poll_stats base;
+    if( more ) {
+      /* the next chunk's counters start where this one's will end: they
+       * are rebased when this one completes */
+      memset(&base, 0, sizeof(base));
+      k = n - issued < p->cfg.evs_per_poll ? n - issued : p->cfg.evs_per_poll;
+      sub_rc = chunk_submit(p, nx, evs + issued, k, &base);
+    }
+    rc = chunk_complete(p, c, stats);
+    if( rc < 0 ) {
+      if( more && sub_rc == 0 && nx->busy ) {  /* it must not outlive the call */
+        (void)oo_gpu_rx_wait(p->gpu, nx->ticket);
+        nx->busy = 0;
+      }
+      return done > 0 ? (int)done : rc;
+    }
+    done += c->n;
+    if( !more )
+      return (int)done;
+    if( sub_rc < 0 )
+      return done > 0 ? (int)done : sub_rc;
+    /* rebase the next chunk's counters on everything completed so far */
+    {
+      uint64_t* a = (uint64_t*)&nx->st;
+      const uint64_t* s = (const uint64_t*)stats;
+      size_t j;
+      for( j = 0; j < sizeof(oo_rx_poll_stats) / sizeof(uint64_t); ++j )
+        a[j] += s[j];
+    }
+    issued += k;
+    cur ^= 1;
   }
-  return (int)n;
 }

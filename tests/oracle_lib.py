@@ -42,6 +42,8 @@ def oracle():
             "oo_or_sock_set": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_abi.Sock)]),
             "oo_or_dump": (_U32, [_P, _P, _U32]),
             "oo_or_rx_one": (None, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
+            "oo_or_walk4": (ctypes.c_int, [_P, _U32, _U32, _U32, _U32, _U32, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.POINTER(_I32)]),
             "oo_or_rx_batch": (None, [_P, _P, ctypes.c_uint64, _P, _U32, _P, ctypes.c_int]),
             "oo_or_ip4_hdr_ok": (ctypes.c_int, [_P, ctypes.c_int]),
             "oo_or_udp4_ok": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t]),
@@ -156,6 +158,14 @@ class OracleStack:
         rows = np.zeros((n, 6), dtype=np.int64)
         self._lib.oo_or_dump(self._t, rows.ctypes.data, n)
         return rows
+
+    def walk4(self, laddr_be, lport_be, raddr_be, rport_be, proto, intf_i=0, vlan=0, stop=False):
+        """One IPv4 lookup stage (ci_netif_filter_for_each_match restated):
+        (match count, first socket id or -1)."""
+        first = ctypes.c_int32(-1)
+        n = self._lib.oo_or_walk4(self._t, laddr_be, lport_be, raddr_be, rport_be, proto, intf_i,
+                                  vlan, int(stop), ctypes.byref(first))
+        return n, first.value
 
     def load_world(self, filters, socks):
         for i, s in enumerate(socks):

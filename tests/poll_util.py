@@ -60,8 +60,41 @@ class Recorder:
 
 
 def in_pool(e, buf_size, pool_bytes):
+    """The frame lies inside its own buffer of the pool."""
     off = int(e["rq_id"]) * buf_size + int(e["ofs"])
-    return int(e["ofs"]) < buf_size and off + int(e["len"]) <= pool_bytes
+    return int(e["ofs"]) + int(e["len"]) <= buf_size and off + int(e["len"]) <= pool_bytes
+
+
+def udp_pre_future(stages):
+    """ci_udp_handle_rx_pre_future (udp_internal.h:58-103) over the matches of
+    its two lookups -- (laddr, lport, raddr, rport) then (laddr, lport), each
+    a list of socket ids in walk order -- with ci_udp_rx_deliver_to_future
+    (:41-52) as the callback, every recvq having room (a full one is the
+    declined-future case): the socket the future resolves, or None."""
+    sock = None
+    for matches in stages:
+        dealt = False
+        for s in matches:
+            if sock is not None:  # :47-50 a second socket: give the future up
+                sock = None
+                dealt = True
+                break
+            sock = s              # :52-53 keep walking for another
+        if dealt:                 # the walk returned 1: stage 2 is skipped (:93-97)
+            break
+    return sock
+
+
+def udp_stage_matches(oracle, r, intf_i):
+    """The two IPv4 UDP lookups of a record's packet, on the oracle's tables
+    (ci_netif_filter_for_each_match restated): lists of socket ids with the
+    first one known (only the first and the count matter to the rule)."""
+    out = []
+    for ra, rp in ((int(r["saddr_be"]), int(r["sport_be"])), (0, 0)):
+        n, first = oracle.walk4(int(r["daddr_be"]), int(r["dport_be"]), ra, rp, 17, intf_i,
+                                int(r["vlan"]))
+        out.append([first] + [-2] * (n - 1) if n else [])
+    return out
 
 
 def transformed(e, sw_verify, buf_size, pool_bytes) -> bool:
@@ -72,16 +105,20 @@ def transformed(e, sw_verify, buf_size, pool_bytes) -> bool:
     return bool(int(e["discard"]) & CSUM_CLASS and ok)
 
 
-def expect(evs, recs, pool, buf_size, sw_verify, decline):
+def expect(evs, recs, pool, buf_size, sw_verify, decline, oracle):
     """The calls and counters the reference loop would produce.  recs: the
-    oracle's records of the transformed events, in event order."""
+    oracle's records of the transformed events, in event order; oracle: an
+    OracleStack holding the same tables (the UDP future rule walks them).
+    rx_evs of the events handed back (other_ev) is the caller loop's to count
+    (netif_event.c:1718), not the shim's."""
     st = Counter()
     calls = []
     k = 0
     for e in evs:
         i, d = int(e["rq_id"]), int(e["discard"])
         if d == 0:
-            st["rx_evs"] += 1
+            if transformed(e, sw_verify, buf_size, pool.nbytes):
+                st["rx_evs"] += 1
         elif d & poll.DISCARD_ETH_LEN_ERR:
             st["rx_discard_len_err"] += 1
         elif d & poll.DISCARD_ETH_FCS_ERR:
@@ -113,10 +150,16 @@ def expect(evs, recs, pool, buf_size, sw_verify, decline):
         pre_l3 = 18 if r["flags"] & _abi.F_VLAN else 14
         if not is6 and r["l4_off"] > pre_l3 + 20:
             st["ip_options"] += 1
-        fut = (not is6 and reason == _abi.R_DELIVER and
-               ((r["proto"] == 6 and r["stage"] == 1) or
-                (r["proto"] == 17 and not r["flags"] & (_abi.F_MCAST | _abi.F_MULTI)
-                 and r["nmatch"] == 1)))
+        # The future seam (IPv4 only): TCP's pre-future walks stage 1 alone
+        # (tcp_rx.h:150-184); UDP's walks both stages with the give-up rule.
+        fut = False
+        if not is6 and reason in (_abi.R_DELIVER, _abi.R_NO_MATCH):
+            if r["proto"] == 6:
+                fut = reason == _abi.R_DELIVER and r["stage"] == 1
+            elif r["proto"] == 17:
+                sock = udp_pre_future(udp_stage_matches(oracle, r, int(e["intf_i"])))
+                fut = sock is not None
+                assert not fut or sock == int(r["sock"]), (sock, r)
         if fut and not decline(i):
             frame = pool[int(e["rq_id"]) * buf_size + int(e["ofs"]):]
             l4 = int(r["l4_off"])

@@ -30,15 +30,16 @@ def cuda():
 
 
 def _oracle_records(frames, evs, pool, sw_verify):
-    """The oracle's records of the events the transform takes, in order."""
+    """The oracle's records of the events the transform takes, in order, and
+    the oracle (its tables hold the edge world)."""
     sel = [(frames[int(e["rq_id"])][0], int(e["intf_i"])) for e in evs
            if transformed(e, sw_verify, BUF, pool.nbytes)]
     o = OracleStack(intf_hwport=HWPORTS)
     install(o, edge_world())
     if not sel:
-        return np.zeros(0, _abi.RESULT_DTYPE)
+        return np.zeros(0, _abi.RESULT_DTYPE), o
     buf, desc = pack(sel)
-    return o.handle_rx_batch(buf, desc)
+    return o.handle_rx_batch(buf, desc), o
 
 
 @pytest.mark.parametrize("sw_verify,evs_per_poll,seed", [(1, 64, 1), (1, 1000, 2), (0, 64, 3),
@@ -57,8 +58,8 @@ def test_poll_dispatch_and_counters(cuda, sw_verify, evs_per_poll, seed):
     rec = Recorder(decline)
     p = poll.RxPoll(g, pool, BUF, evs_per_poll, bool(sw_verify), rec)
     assert p.poll(evs) == len(evs)
-    want_recs = _oracle_records(frames, evs, pool, sw_verify)
-    calls, want = expect(evs, want_recs, pool, BUF, sw_verify, decline)
+    want_recs, o = _oracle_records(frames, evs, pool, sw_verify)
+    calls, want = expect(evs, want_recs, pool, BUF, sw_verify, decline, o)
     # the records the callbacks saw are the oracle's, bit for bit
     got = np.array([tuple(r[k] for k in _abi.RESULT_DTYPE.names) for r in rec.recs],
                    dtype=_abi.RESULT_DTYPE)

@@ -190,3 +190,43 @@ def test_import_replicates_tables(cuda):
     for f in filters[::7][:50]:
         a = _raw(f)[1:]
         assert g.filter_lookup_raw(*a) == o.filter_lookup_raw(*a)
+
+
+def _run_streams(torch, nstreams, nlaunch, cfg, n, done_every=0):
+    filters, socks = pktgen.world(cfg)
+    g = GpuRxStack(device=0)
+    o = OracleStack()
+    for st in (g, o):
+        st.load_world(filters, socks)
+    buf, desc = pktgen.generate(cfg, n, first=31)
+    fr, de = to_dev(buf), to_dev(desc)
+    want = o.handle_rx_batch(buf, desc, nthreads=8)
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    outs = [torch.full((n * 32,), 0xAB, dtype=torch.uint8, device="cuda") for _ in range(nlaunch)]
+    torch.cuda.synchronize()
+    for i in range(nlaunch):
+        s = streams[i % nstreams]
+        g.handle_rx_batch_dev(fr.data_ptr(), fr.numel(), de.data_ptr(), n, outs[i].data_ptr(), 0,
+                              s.cuda_stream)
+        if done_every and i % done_every == done_every - 1:
+            g.stream_done(s.cuda_stream)
+            streams[i % nstreams] = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for i, out in enumerate(outs):
+        got = out.cpu().numpy().view(_abi.RESULT_DTYPE)
+        assert got.tobytes() == want.tobytes(), f"launch {i}: " + diff_report(got, want, desc)
+    g.close()
+
+
+def test_launches_on_three_streams_share_no_claim_counters(cuda):
+    """24 launches queued round-robin on three streams run
+    concurrently; each stream has its own tile-claim counters, so every launch
+    claims every tile exactly once (short frames: many claims per us)."""
+    _run_streams(cuda, 3, 24, 3, 1 << 18)
+
+
+def test_more_streams_than_tracked_entries(cuda):
+    """Eleven streams through the context's eight tracked entries (a reused
+    entry's new stream waits for the old one), with streams given up by
+    oo_gpu_rx_stream_done and replaced as they go."""
+    _run_streams(cuda, 11, 33, 2, 1 << 16, done_every=5)

@@ -61,7 +61,7 @@ def test_untransformed_events_follow_the_loop():
     rec = Recorder()
     p = poll.RxPoll(st, pool, 2048, 64, True, rec)
     assert p.poll(evs) == len(evs)
-    calls, want = expect(evs, [], pool, 2048, True, lambda i: False)
+    calls, want = expect(evs, [], pool, 2048, True, lambda i: False, None)
     assert rec.calls == calls
     assert onload_stats(p.stats.as_dict()) == want
     assert p.stats.n_batches == 0
@@ -81,9 +81,50 @@ def test_device_failure_runs_no_callback():
     # with sw_verify off the same plain events are the loop's own business
     q = poll.RxPoll(st, pool, 2048, 4, False, rec)
     assert q.poll(evs) == len(evs)
-    assert rec.calls == [("other", i) for i in range(10)] and q.stats.rx_evs == 10
+    # ... and their rx_evs is the loop's to count (not twice)
+    assert rec.calls == [("other", i) for i in range(10)] and q.stats.rx_evs == 0
     p.close()
     q.close()
+    st.close()
+
+
+def test_failure_after_a_handled_chunk_returns_the_handled_count():
+    """Chunks of 4: the first holds only events the transform does not take
+    (its callbacks run, its counters land), the second needs the device,
+    which fails: the call returns 4 and the caller still owns events 4.."""
+    rng = np.random.default_rng(9)
+    pool, evs = events_for([(bytes(80), 0)] * 8, 2048, rng, discard_mix=False)
+    evs["flags"][:4] = poll.EV_SOP | poll.EV_CONT  # multi-buffer: the loop's own
+    evs["discard"][2] = poll.DISCARD_ETH_FCS_ERR    # a discard outside the csum class
+    st = GpuRxStack(device=-1)
+    rec = Recorder()
+    p = poll.RxPoll(st, pool, 2048, 4, True, rec)
+    assert p.poll(evs) == 4
+    assert rec.calls == [("other", 0), ("other", 1), ("release", 2, None), ("other", 3)]
+    d = p.stats.as_dict()
+    assert d["rx_discard_crc_bad"] == 1 and d["n_other"] == 3 and d["rx_evs"] == 0
+    p.close()
+    st.close()
+
+
+def test_frame_past_its_buffer_is_not_taken():
+    """an event whose frame runs past the end of its buffer (ofs +
+    len > buf_size) is not the shim's: a plain event goes back to the loop,
+    a checksum-class discard is released -- never copied into a gather slot."""
+    pool = np.zeros(8 * 2048, np.uint8)
+    evs = np.zeros(3, poll.EV_DTYPE)
+    evs[0] = (0, 1000, 1100, poll.EV_SOP, 0, 0, 0)                          # 2100 > 2048
+    evs[1] = (1, 2047, 2, poll.EV_SOP, poll.DISCARD_L4_CSUM_ERR, 0, 0)     # 2049 > 2048
+    evs[2] = (2, 192, 1856, poll.EV_SOP, 0, 0, 0)                           # 2048: fits
+    st = GpuRxStack(device=-1)
+    rec = Recorder()
+    p = poll.RxPoll(st, pool, 2048, 64, True, rec)
+    # event 2 fits its buffer exactly and needs the device: the host-only
+    # context fails that batch, so only a call over the first two completes
+    assert p.poll(evs[:2]) == 2
+    assert rec.calls == [("other", 0), ("release", 1, None)]
+    assert p.poll(evs[2:]) == -19
+    p.close()
     st.close()
 
 
