@@ -81,6 +81,9 @@ def parse_args(argv=None):
     ap.add_argument("--pipelined", action="store_true",
                     help="also time consecutive batches alternating over two streams (a side "
                          "measurement: never value)")
+    ap.add_argument("--table-ops", action="store_true",
+                    help="also time device-side table maintenance: the world load's flush, "
+                         "and a 100-op filter churn batch in front of one batch")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-memory path: oo_gpu_rx_submit/_wait, pinned "
                          "double-buffered H2D + transform + D2H")
@@ -95,22 +98,46 @@ def _free_port() -> int:
     return p
 
 
-def launch_ranks(n: int, argv: list[str]) -> int:
+def launch_ranks(n: int, argv: list[str], script: str | None = None,
+                 poll_s: float = 0.2, grace_s: float = 10.0) -> int:
     """Start n ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE /
     MASTER_* set, one GPU each) as child processes -- this process never
-    touches a GPU -- and return the worst exit status."""
+    touches a GPU -- and return the worst exit status.
+
+    Watchdog: the children are polled together; the first one to exit
+    non-zero gets the others terminated (SIGTERM, then SIGKILL after
+    grace_s) -- they would otherwise block in a barrier or an RCCL
+    collective until an outer timeout -- and its status is returned, with
+    the rank named on stderr."""
     port = str(_free_port())
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv,
                                       env=env))
-    rc = 0
-    for p in procs:
-        c = p.wait()
-        rc = c if rc == 0 else rc
-    return rc
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0:
+                log(f"bench.py: rank {r} exited with status {c}; stopping ranks {sorted(live)}")
+                for k in live:
+                    procs[k].terminate()
+                deadline = time.time() + grace_s
+                for k in live:
+                    try:
+                        procs[k].wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        procs[k].kill()
+                        procs[k].wait()
+                return c
+        if live:
+            time.sleep(poll_s)
+    return 0
 
 
 def main(argv=None) -> int:
@@ -276,6 +303,9 @@ def run_rank(args) -> None:
         extras["pipelined_2stream"] = time_pipelined(torch, stack, frames, d_desc, n, my_mean, out,
                                                      dev, stream, args.steps, args.warmup)
         log(f"[rank {rank}] pipelined: {json.dumps(extras['pipelined_2stream'])}")
+    if args.table_ops:
+        extras["table_ops"] = time_table_ops(torch, filters, socks, frames, d_desc, n, out, local)
+        log(f"[rank {rank}] table ops: {json.dumps(extras['table_ops'])}")
     if args.host_path:
         extras["host_path"] = time_host_path(torch, filters, socks, buf, desc, local)
         log(f"[rank {rank}] host path: {json.dumps(extras['host_path'])}")
@@ -524,6 +554,58 @@ def time_pipelined(torch, stack, frames, d_desc, n, mean_len, out, dev, stream, 
     gbs = (mean_len + DESC_B + RESULT_B) * n / (ms * 1e-3) / 1e9
     return {"ms_per_batch": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 2),
             "achieved_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "streams": 2}
+
+
+def time_table_ops(torch, filters, socks, frames, d_desc, n, out, device, reps=5):
+    """Device-side table maintenance: the flush of a
+    whole world load (every socket record and filter insert: the ops the
+    stack's start-up queues), and a churn batch of 100 ops (50 filters
+    removed and re-inserted) flushed in front of one batch, against the
+    batch alone.  Event-timed on the stream; a side measurement."""
+    from onload_amd.rx import GpuRxStack
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return float(e0.elapsed_time(e1))
+
+    loads = []
+    for _ in range(reps):
+        g = GpuRxStack(device=device)
+        g.load_world(filters, socks)  # queued on the host
+        loads.append(timed(lambda: g.sync(sh)))
+        g.close()
+    g = GpuRxStack(device=device)
+    g.load_world(filters, socks)
+    g.sync(sh)
+    churn = [f for f in filters if f.af == 4][:50]
+
+    def batch():
+        g.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
+                              out.data_ptr(), 0, sh)
+
+    def churn_and_batch():
+        for f in churn:
+            ra = None if f.raddr_any else bytes(f.raddr)[:4]
+            g.filter_remove_raw(f.sock, 4, bytes(f.laddr)[:4], f.lport_be, ra, f.rport_be, f.proto)
+        for f in churn:
+            ra = None if f.raddr_any else bytes(f.raddr)[:4]
+            g.filter_insert_raw(f.sock, 4, bytes(f.laddr)[:4], f.lport_be, ra, f.rport_be, f.proto)
+        batch()
+    for _ in range(3):
+        batch()
+    alone = sorted(timed(batch) for _ in range(reps))
+    with_churn = sorted(timed(churn_and_batch) for _ in range(reps))
+    g.close()
+    return {"world_ops": len(filters) + len(socks), "world_flush_ms": round(sorted(loads)[reps // 2], 4),
+            "churn_ops": 2 * len(churn), "batch_ms": round(alone[reps // 2], 4),
+            "churn_plus_batch_ms": round(with_churn[reps // 2], 4)}
 
 
 def time_host_path(torch, filters, socks, buf, desc, device, batch=1 << 16, reps=3):

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <new>
+#include <unordered_map>
 #include <vector>
 
 #include "oo_rx_device.h"
@@ -36,7 +37,8 @@ extern "C" int oo_rx_launch_short(const oo_rx::KParams* P, int grid, hipStream_t
 extern "C" int oo_rx_blocks_per_cu_short(void);
 extern "C" int oo_rx_waves_per_block(void);
 extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
-                                   uint32_t n, uint32_t gen, hipStream_t s);
+                                   const uint32_t* d_lev_end, uint32_t nlev, uint32_t gen,
+                                   hipStream_t s);
 extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s);
 extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s);
 extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s);
@@ -167,6 +169,17 @@ struct oo_gpu_rx_ctx {
   DevTables T = {};
   std::vector<TableOp> ops;
   bool ops_sock = false;  // ops holds an OP_SOCK (a refresh pass follows)
+  // Parallel application (table_ops): each pending op's level -- one more
+  // than the highest level of an earlier pending op that touched any slot
+  // it touches (the probe walk the mirror just did) -- so ops of one level
+  // touch disjoint slots and commute; levels run in order.  Socket ops are
+  // level 0 (the refresh pass rewrites every slot of a changed socket after
+  // all of them), and a later op on the same socket supersedes an earlier
+  // one.
+  std::vector<uint32_t> op_level;
+  std::unordered_map<uint64_t, uint32_t> slot_level;  // (af << 32 | slot) -> first free level
+  std::unordered_map<int32_t, size_t> sock_op_at;     // socket id -> its pending OP_SOCK
+  std::vector<uint32_t> touched;                      // the last mirror op's probe walk
   uint32_t gen = 1;       // flush generation (sockgen marks)
   uint32_t tables_gen = 0;  // flushes done; streams wait for it via tables_ev
   hipEvent_t tables_ev = nullptr;
@@ -202,10 +215,35 @@ namespace {
 
 bool has_dev(const oo_gpu_rx_ctx* c) { return c->device >= 0; }
 
+// Queues op for the device.  A table op's level comes from the slots its
+// mirror walk touched (c->touched); a socket op supersedes the socket's
+// pending one.
 void push_op(oo_gpu_rx_ctx* c, const TableOp& op) {
   if (!has_dev(c)) return;
+  uint32_t level = 0;
+  if (op.kind == oo_rx::OP_SOCK) {
+    c->ops_sock = true;
+    auto it = c->sock_op_at.find(op.sock);
+    if (it != c->sock_op_at.end()) c->ops[it->second].kind = 0;  // superseded: skipped
+    c->sock_op_at[op.sock] = c->ops.size();
+  } else {
+    const uint64_t af = (uint64_t)op.af << 32;
+    for (uint32_t slot : c->touched) {
+      auto it = c->slot_level.find(af | slot);
+      if (it != c->slot_level.end()) level = std::max(level, it->second);
+    }
+    for (uint32_t slot : c->touched) c->slot_level[af | slot] = level + 1;
+  }
   c->ops.push_back(op);
-  if (op.kind == oo_rx::OP_SOCK) c->ops_sock = true;
+  c->op_level.push_back(level);
+}
+
+void clear_ops(oo_gpu_rx_ctx* c) {
+  c->ops.clear();
+  c->op_level.clear();
+  c->slot_level.clear();
+  c->sock_op_at.clear();
+  c->ops_sock = false;
 }
 
 TableOp tuple_op(uint8_t kind, int af, const void* la, uint16_t lp, const void* ra, uint16_t rp,
@@ -225,16 +263,20 @@ TableOp tuple_op(uint8_t kind, int af, const void* la, uint16_t lp, const void* 
 }
 
 // ---- IPv4 mirror: netif_table.c:323-495.
+// Each mirror op leaves the slots its walk touched in c->touched.
 int ip4_insert(oo_gpu_rx_ctx* c, int32_t id, uint32_t la, uint32_t lp, uint32_t ra,
                uint32_t rp, uint32_t proto) {
   uint32_t h1 = hash3(la, lp, ra, rp, proto) & c->ip4_mask;
   const uint32_t h2 = hash2(la, lp, ra, rp, proto);
   const uint32_t first = h1;
+  c->touched.clear();
   while (occupied(c->ip4[h1].id_state)) {
+    c->touched.push_back(h1);
     ++c->ip4_ext[h1].route_count;
     h1 = (h1 + h2) & c->ip4_mask;
     if (h1 == first) return -ENOBUFS;  // route counts stay raised (:349-376)
   }
+  c->touched.push_back(h1);
   c->ip4[h1].id_state = (h1 == first ? ST_PREFERRED : ST_REHASHED) | ((uint32_t)id & ID_MASK);
   c->ip4[h1].laddr = la;
   c->ip4_ext[h1].lport = (uint16_t)lp;
@@ -247,7 +289,9 @@ void ip4_remove(oo_gpu_rx_ctx* c, int32_t id, uint32_t la, uint32_t lp, uint32_t
   const uint32_t h2 = hash2(la, lp, ra, rp, proto);
   uint32_t i = h1;
   int hops = 0;
+  c->touched.clear();
   for (;;) {
+    c->touched.push_back(i);
     const uint32_t st = c->ip4[i].id_state;
     if (occupied(st) && (st & ID_MASK) == ((uint32_t)id & ID_MASK)) {
       if (la == c->ip4[i].laddr) break;
@@ -296,11 +340,14 @@ int ip6_insert(oo_gpu_rx_ctx* c, int32_t id, const uint8_t* la, uint32_t lp,
   uint32_t h1 = hash3(lx, lp, rx, rp, proto) & c->ip6_mask;
   const uint32_t h2 = hash2(lx, lp, rx, rp, proto);
   const uint32_t first = h1;
+  c->touched.clear();
   while (c->ip6[h1].id >= 0) {
+    c->touched.push_back(h1);
     ++c->ip6[h1].route_count;
     h1 = (h1 + h2) & c->ip6_mask;
     if (h1 == first) return -ENOBUFS;
   }
+  c->touched.push_back(h1);
   c->ip6[h1].id = id;
   memcpy(c->ip6[h1].laddr, la, 16);
   return 0;
@@ -313,7 +360,9 @@ void ip6_remove(oo_gpu_rx_ctx* c, int32_t id, const uint8_t* la, uint32_t lp,
   const uint32_t h2 = hash2(lx, lp, rx, rp, proto);
   uint32_t i = h1;
   int hops = 0;
+  c->touched.clear();
   for (;;) {
+    c->touched.push_back(i);
     const Entry6& e = c->ip6[i];
     if (e.id == id) {
       if (memcmp(la, e.laddr, 16) == 0) break;
@@ -560,7 +609,13 @@ int order_after_batches(oo_gpu_rx_ctx* c, hipStream_t s) {
 int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
   if (c->ops.empty()) return 0;
   if (order_after_batches(c, s) != 0) return -EIO;
+  // The ops in level order (call order within a level), cut into chunks;
+  // each chunk carries the end of every level it holds part of.
   const uint32_t total = (uint32_t)c->ops.size();
+  std::vector<uint32_t> order(total);
+  for (uint32_t i = 0; i < total; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(),
+                   [c](uint32_t a, uint32_t b) { return c->op_level[a] < c->op_level[b]; });
   for (uint32_t at = 0; at < total; at += OPS_CHUNK) {
     const uint32_t n = std::min(OPS_CHUNK, total - at);
     OpStage& st = c->stage[c->stage_next];
@@ -569,9 +624,20 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
       c->failed = at > 0;
       return -EIO;
     }
-    memcpy(st.h, c->ops.data() + at, sizeof(TableOp) * n);
+    TableOp* h = st.h;
+    uint32_t* lev_end = reinterpret_cast<uint32_t*>(h + OPS_CHUNK);
+    uint32_t nlev = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint32_t i = order[at + k];
+      h[k] = c->ops[i];
+      if (k > 0 && c->op_level[i] != c->op_level[order[at + k - 1]]) lev_end[nlev++] = k;
+    }
+    lev_end[nlev++] = n;
     if (hipMemcpyAsync(st.d, st.h, sizeof(TableOp) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-        oo_table_launch_ops(&c->T, st.d, n, c->gen, s) != 0 ||
+        hipMemcpyAsync(st.d + OPS_CHUNK, lev_end, sizeof(uint32_t) * nlev, hipMemcpyHostToDevice,
+                       s) != hipSuccess ||
+        oo_table_launch_ops(&c->T, st.d, reinterpret_cast<const uint32_t*>(st.d + OPS_CHUNK), nlev,
+                            c->gen, s) != 0 ||
         hipEventRecord(st.ev, s) != hipSuccess) {
       c->failed = true;  // this chunk or an earlier one may have reached the device
       return -EIO;
@@ -582,8 +648,7 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
     c->failed = true;
     return -EIO;
   }
-  c->ops.clear();
-  c->ops_sock = false;
+  clear_ops(c);
   ++c->gen;
   ++c->tables_gen;
   Tracked* t = track_of(c, s);
@@ -730,8 +795,9 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
       oo_table_launch_init(&T, c->stream) == 0;
   for (OpStage& st : c->stage)
-    ok = ok && hipHostMalloc(&st.h, sizeof(TableOp) * OPS_CHUNK, hipHostMallocDefault) == hipSuccess &&
-         hipMalloc(&st.d, sizeof(TableOp) * OPS_CHUNK) == hipSuccess &&
+    ok = ok && hipHostMalloc(&st.h, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK,
+                             hipHostMallocDefault) == hipSuccess &&
+         hipMalloc(&st.d, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK) == hipSuccess &&
          hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) == hipSuccess;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
@@ -910,8 +976,7 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, vo
   }
   // Setup-time call: the image comes to the host once for the mirror, and
   // the device arrays are copied on the stream after every earlier use.
-  c->ops.clear();
-  c->ops_sock = false;
+  clear_ops(c);
   if (order_after_batches(c, s) != 0) return -EIO;
   if (hipMemcpyAsync(host.data(), src, h.total, hipMemcpyDefault, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)

@@ -23,9 +23,13 @@
 // every slot that names a marked socket -- an O(table) pass, but a GPU one
 // (2^16 + 2^14 slots) on the stream, not a host rescan.
 //
-// Table ops are rare next to batches (filter churn), and their order
-// matters, so table_ops is one wave walking the ops in order; its lane 0
-// does the probe walks (each step one dependent load, as on the CPU).
+// The ops of a flush arrive in levels (oo_gpu_rx.cpp push_op): the ops of
+// one level touch disjoint slots -- the probe walks the host mirror did for
+// them -- so they commute, and table_ops applies a level one op per lane,
+// the levels in order with a workgroup barrier between them.  Socket-field
+// ops are all level 0 (one per socket: the last change wins), and the
+// refresh pass that follows rewrites every slot of a changed socket, so
+// when an insert reads a socket's fields does not matter.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,9 +38,13 @@
 
 namespace oo_rx {
 
+// Ops of one level touch disjoint slots but may share an occupancy word.
 __device__ __forceinline__ void occ_set(uint32_t* occ, uint32_t i, bool on) {
   const uint32_t b = 1u << (i & 31u);
-  occ[i >> 5] = on ? (occ[i >> 5] | b) : (occ[i >> 5] & ~b);
+  if (on)
+    atomicOr(&occ[i >> 5], b);
+  else
+    atomicAnd(&occ[i >> 5], ~b);
 }
 
 // The socket fields of slot records (what netif_table.c:192-231 reads through
@@ -200,23 +208,31 @@ __device__ void ip6_remove(const DevTables& T, const TableOp& op) {
   set_id(i, T.slot6[i].route_count == 0 ? ID6_EMPTY : ID6_TOMBSTONE);
 }
 
-// The ops of one flush, in order.  One wave; lane 0 works.
-__global__ __launch_bounds__(64) void table_ops(DevTables T, const TableOp* ops, uint32_t n,
-                                                uint32_t gen) {
-  if (threadIdx.x != 0) return;
-  for (uint32_t k = 0; k < n; ++k) {
-    const TableOp op = ops[k];
-    if (op.sock < 0 || (uint32_t)op.sock >= T.max_socks) continue;  // the host rejected it
-    if (op.kind == OP_SOCK) {
-      T.socks[op.sock] = op.u.s;
-      T.sockgen[op.sock] = gen;
-    } else if (op.kind == OP_INSERT) {
-      if (op.af == 4) ip4_insert(T, op);
-      else ip6_insert(T, op);
-    } else if (op.kind == OP_REMOVE) {
-      if (op.af == 4) ip4_remove(T, op);
-      else ip6_remove(T, op);
-    }
+__device__ __forceinline__ void apply_op(const DevTables& T, const TableOp& op, uint32_t gen) {
+  if (op.sock < 0 || (uint32_t)op.sock >= T.max_socks) return;  // the host rejected it
+  if (op.kind == OP_SOCK) {
+    T.socks[op.sock] = op.u.s;
+    T.sockgen[op.sock] = gen;
+  } else if (op.kind == OP_INSERT) {
+    if (op.af == 4) ip4_insert(T, op);
+    else ip6_insert(T, op);
+  } else if (op.kind == OP_REMOVE) {
+    if (op.af == 4) ip4_remove(T, op);
+    else ip6_remove(T, op);
+  }  // kind 0: a socket op superseded by a later one
+}
+
+// The ops of one flush chunk: level L is ops[lev_end[L-1], lev_end[L]).
+constexpr int TABLE_THREADS = 1024;
+__global__ __launch_bounds__(TABLE_THREADS) void table_ops(DevTables T, const TableOp* ops,
+                                                           const uint32_t* lev_end, uint32_t nlev,
+                                                           uint32_t gen) {
+  uint32_t start = 0;
+  for (uint32_t L = 0; L < nlev; ++L) {
+    const uint32_t end = lev_end[L];
+    for (uint32_t k = start + threadIdx.x; k < end; k += TABLE_THREADS) apply_op(T, ops[k], gen);
+    __syncthreads();  // the next level sees this one's slots
+    start = end;
   }
 }
 
@@ -302,8 +318,10 @@ int grid_for(uint32_t items) {
 }  // namespace
 
 extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
-                                   uint32_t n, uint32_t gen, hipStream_t s) {
-  hipLaunchKernelGGL(oo_rx::table_ops, dim3(1), dim3(64), 0, s, *T, d_ops, n, gen);
+                                   const uint32_t* d_lev_end, uint32_t nlev, uint32_t gen,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(oo_rx::table_ops, dim3(1), dim3(oo_rx::TABLE_THREADS), 0, s, *T, d_ops,
+                     d_lev_end, nlev, gen);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1,0 +1,374 @@
+/* SPDX-License-Identifier: BSD-2-Clause */
+/*
+ * ref_l4_harness.c -- TEST INFRASTRUCTURE ONLY.  Runs the reference's own
+ * receive path for one frame at a time -- handle_rx_csum_bad, handle_rx_pkt
+ * and ci_parse_rx_vlan (src/lib/transport/ip/netif_event.c, #included below
+ * to reach its statics), ci_udp_handle_rx (udp_rx.c) and ci_tcp_handle_rx
+ * (tcp_rx.c), the filter tables (netif_table.c, netif_table_ip6.c) and the
+ * checksum code (ciul/checksum.c, citools/ip_csum_partial.c), all compiled
+ * unmodified by oracle/Makefile -- to generate the fixtures that pin the
+ * oracle's and the kernel's gates, lookup stages and future rules
+ * (tests/golden/make_l4_golden.py).  This is SURVEY.md Appendix A's recipe.
+ *
+ * Linked as the reference links its unit tests (src/tests/unit/mmake.mk:
+ * 80-99: non-PIE, --unresolved-symbols=ignore-all, the object under test
+ * plus harness definitions of the functions it calls out to, as its
+ * lib/transport/ip/tcp_rx.c unit test defines ci_netif_filter_for_each_match
+ * and ci_netif_pkt_pass_to_kernel).  Here the lookups are the REAL table
+ * walks, observed through ld --wrap:
+ *   __wrap_ci_netif_filter_for_each_match[_ip6]
+ *       count mode (the full handlers): runs the real walk with a counting
+ *       callback, records {matches, first socket} per lookup stage and the
+ *       stage-1 hash, and plays the deliver callback's part for the stage
+ *       that matched -- TCP: rxp->pkt = NULL, UDP: state->delivered = 1 --
+ *       returning 1 as the real callbacks do (tcp_rx.c:4644-4657,
+ *       udp_rx.c:141-228);
+ *       pass-through mode (the futures): the real walk with the caller's own
+ *       callback (ci_udp_rx_deliver_to_future, ci_tcp_rx_deliver_to_future).
+ *   __wrap_ci_udp_handle_rx / __wrap_ci_tcp_handle_rx
+ *       record the L4 entry (offset, ip_paylen), run the real pre-future
+ *       (udp_internal.h:58-103 / tcp_rx.h:150-184) in pass-through mode for
+ *       an IPv4 packet, then the real handler in count mode.
+ *   ci_netif_pkt_pass_to_kernel: records "kernel", returns 1.
+ * Hidden (CI_HF) symbols the link cannot leave unresolved get
+ * __builtin_trap() bodies generated from the linker's own list
+ * (oracle/Makefile): none is reached -- reaching one kills the harness.
+ *
+ * Script (stdin), one command per line; every command prints one line:
+ *   I log4 log6 nsocks nintf hwport0 ...        init (as ref_table_harness)
+ *   S id af proto lport rport raddr flags hwports vlan
+ *   A af sock laddr lport raddr rport proto     ci_netif_filter_insert
+ *   P intf hexframe                             one frame ->
+ *     "r handled kernel entry l4off ip_paylen n1 f1 n2 f2 n3 f3 hash fut"
+ *     entry 0: no L4 handler ran, else 6 / 17; nK fK per lookup stage K the
+ *     handler ran (-1 -1 if it did not); hash: stage-1 hash_out (TCP);
+ *     fut: the pre-future's socket (-1 none, -2 not run).
+ */
+#include "netif_event.c"                  /* -I src/lib/transport/ip */
+#include "udp_internal.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static ci_netif ni_;
+static ci_netif* ni = &ni_;
+static int nsocks_;
+
+/* ---- the record of one frame */
+static struct {
+  int kernel, entry, l4off, ip_paylen, stage, fut;
+  int n[3], first[3];
+  unsigned hash;
+} R;
+static int g_passthrough;
+
+static void hexbytes(const char* s, unsigned char* out, int n)
+{
+  int i;
+  memset(out, 0, n);
+  if( s[0] == '-' )
+    return;
+  for( i = 0; i < n && s[2 * i] && s[2 * i + 1]; ++i ) {
+    unsigned v;
+    sscanf(s + 2 * i, "%2x", &v);
+    out[i] = (unsigned char) v;
+  }
+}
+
+static ci_addr_t addr_of(int af, const char* s)
+{
+  ci_addr_t a;
+  memset(&a, 0, sizeof(a));
+  if( af == 6 ) {
+    hexbytes(s, (unsigned char*) a.ip6, 16);
+  }
+  else {
+    unsigned char b[4];
+    ci_uint32 v;
+    hexbytes(s, b, 4);
+    memcpy(&v, b, 4);
+    a = CI_ADDR_FROM_IP4(v);
+  }
+  return a;
+}
+
+static int sock_id(ci_sock_cmn* s)
+{
+  return (int) OO_SP_TO_INT(oo_statep_to_sockp(ni, (oo_p) ((char*) s - (char*) ni->state)));
+}
+
+/* ---- observed lookups */
+struct count { int n; int first; };
+
+static int count_cb(ci_sock_cmn* s, void* arg)
+{
+  struct count* c = arg;
+  if( c->n++ == 0 )
+    c->first = sock_id(s);
+  return 0;
+}
+
+static int stage_done(unsigned proto, struct count* c, void* arg)
+{
+  int k = R.stage++;
+  if( k < 3 ) {
+    R.n[k] = c->n;
+    R.first[k] = c->first;
+  }
+  if( c->n == 0 )
+    return 0;
+  /* what the deliver callback that accepted the packet leaves behind */
+  if( proto == IPPROTO_TCP )
+    ((ciip_tcp_rx_pkt*) arg)->pkt = NULL;
+  else
+    ((struct ci_udp_rx_deliver_state*) arg)->delivered = 1;
+  return 1;
+}
+
+extern int __real_ci_netif_filter_for_each_match(ci_netif*, unsigned, unsigned, unsigned,
+                                                 unsigned, unsigned, int, int,
+                                                 int (*)(ci_sock_cmn*, void*), void*,
+                                                 ci_uint32*);
+int __wrap_ci_netif_filter_for_each_match(ci_netif* n, unsigned la, unsigned lp, unsigned ra,
+                                          unsigned rp, unsigned proto, int intf, int vlan,
+                                          int (*cb)(ci_sock_cmn*, void*), void* arg,
+                                          ci_uint32* hash_out)
+{
+  struct count c = { 0, -1 };
+  ci_uint32 h = 0;
+  if( g_passthrough )
+    return __real_ci_netif_filter_for_each_match(n, la, lp, ra, rp, proto, intf, vlan, cb, arg,
+                                                 hash_out);
+  __real_ci_netif_filter_for_each_match(n, la, lp, ra, rp, proto, intf, vlan, count_cb, &c,
+                                        hash_out ? &h : NULL);
+  if( hash_out ) {
+    *hash_out = h;
+    if( R.stage == 0 )
+      R.hash = h;
+  }
+  return stage_done(proto, &c, arg);
+}
+
+#if CI_CFG_IPV6
+extern int __real_ci_netif_filter_for_each_match_ip6(ci_netif*, const ci_addr_t*, unsigned,
+                                                     const ci_addr_t*, unsigned, unsigned, int,
+                                                     int, int (*)(ci_sock_cmn*, void*), void*,
+                                                     ci_uint32*);
+int __wrap_ci_netif_filter_for_each_match_ip6(ci_netif* n, const ci_addr_t* la, unsigned lp,
+                                              const ci_addr_t* ra, unsigned rp, unsigned proto,
+                                              int intf, int vlan,
+                                              int (*cb)(ci_sock_cmn*, void*), void* arg,
+                                              ci_uint32* hash_out)
+{
+  struct count c = { 0, -1 };
+  ci_uint32 h = 0;
+  if( g_passthrough )
+    return __real_ci_netif_filter_for_each_match_ip6(n, la, lp, ra, rp, proto, intf, vlan, cb,
+                                                     arg, hash_out);
+  __real_ci_netif_filter_for_each_match_ip6(n, la, lp, ra, rp, proto, intf, vlan, count_cb, &c,
+                                            hash_out ? &h : NULL);
+  if( hash_out ) {
+    *hash_out = h;
+    if( R.stage == 0 )
+      R.hash = h;
+  }
+  return stage_done(proto, &c, arg);
+}
+#endif
+
+/* ---- observed L4 entries */
+extern void __real_ci_udp_handle_rx(ci_netif*, ci_ip_pkt_fmt*, ci_udp_hdr*, int);
+void __wrap_ci_udp_handle_rx(ci_netif* n, ci_ip_pkt_fmt* pkt, ci_udp_hdr* udp, int ip_paylen)
+{
+  R.entry = IPPROTO_UDP;
+  R.l4off = (int) ((char*) udp - PKT_START(pkt));
+  R.ip_paylen = ip_paylen;
+  if( oo_pkt_af(pkt) == AF_INET ) {
+    struct ci_udp_rx_future fut;
+    g_passthrough = 1;
+    ci_udp_handle_rx_pre_future(n, pkt, udp, ip_paylen, CI_ETHERTYPE_IP, &fut);
+    g_passthrough = 0;
+    R.fut = fut.socket ? sock_id(&fut.socket->s) : -1;
+  }
+  __real_ci_udp_handle_rx(n, pkt, udp, ip_paylen);
+}
+
+extern void __real_ci_tcp_handle_rx(ci_netif*, struct ci_netif_poll_state*, ci_ip_pkt_fmt*,
+                                    ci_tcp_hdr*, int);
+void __wrap_ci_tcp_handle_rx(ci_netif* n, struct ci_netif_poll_state* ps, ci_ip_pkt_fmt* pkt,
+                             ci_tcp_hdr* tcp, int ip_paylen)
+{
+  R.entry = IPPROTO_TCP;
+  R.l4off = (int) ((char*) tcp - PKT_START(pkt));
+  R.ip_paylen = ip_paylen;
+  if( oo_pkt_af(pkt) == AF_INET ) {
+    struct ci_tcp_rx_future fut;
+    g_passthrough = 1;
+    ci_tcp_handle_rx_pre_future(n, pkt, tcp, ip_paylen, &fut);
+    g_passthrough = 0;
+    R.fut = fut.socket ? sock_id(fut.socket) : -1;
+  }
+  __real_ci_tcp_handle_rx(n, ps, pkt, tcp, ip_paylen);
+}
+
+/* The harness's own definition, as the reference's tcp_rx unit test has. */
+int ci_netif_pkt_pass_to_kernel(ci_netif* n, ci_ip_pkt_fmt* pkt)
+{
+  (void) n;
+  (void) pkt;
+  R.kernel = 1;
+  return 1;
+}
+
+/* ---- setup */
+static void do_init(int log4, int log6, int nsocks, int nintf, int* hw)
+{
+  unsigned n4 = 1u << log4, n6 = 1u << log6, i;
+  size_t state_bytes = (sizeof(ci_netif_state) + 4095) & ~(size_t) 4095;
+  char* base = calloc(1, state_bytes + (size_t) nsocks * EP_BUF_SIZE);
+  ci_netif_state* st = (ci_netif_state*) base;
+  memset(ni, 0, sizeof(*ni));
+  ni->state = st;
+  nsocks_ = nsocks;
+  st->lock.lock = CI_EPLOCK_LOCKED;  /* called under the stack lock */
+  *(ci_uint32*) &st->ep_ofs = (ci_uint32) state_bytes;
+  *(ci_uint32*) &st->n_ep_bufs = (ci_uint32) nsocks;
+  for( i = 0; i < (unsigned) nintf && i < CI_CFG_MAX_INTERFACES; ++i )
+    st->intf_i_to_hwport[i] = (ci_int8) hw[i];
+  ni->filter_table = calloc(1, sizeof(ci_netif_filter_table) +
+                               n4 * sizeof(ci_netif_filter_table_entry_fast));
+  ni->filter_table_ext = calloc(n4, sizeof(ci_netif_filter_table_entry_ext));
+  *(unsigned*) &ni->filter_table->table_size_mask = n4 - 1;
+  for( i = 0; i < n4; ++i )
+    ni->filter_table->table[i].__id_and_state = 2u << 30;  /* EMPTY, id 0 */
+  ni->ip6_filter_table = calloc(1, sizeof(ci_ip6_netif_filter_table) +
+                                   n6 * sizeof(ci_ip6_netif_filter_table_entry));
+  *(unsigned*) &ni->ip6_filter_table->table_size_mask = n6 - 1;
+  for( i = 0; i < n6; ++i )
+    ni->ip6_filter_table->table[i].id = -2;               /* EMPTY */
+  printf("ok\n");
+}
+
+static void do_sock(int id, int af, int proto, unsigned lport, unsigned rport,
+                    const char* raddr, unsigned flags, unsigned long long hwports, int vlan)
+{
+  ci_sock_cmn* s = ID_TO_SOCK(ni, id);
+  memset(s, 0, EP_BUF_SIZE);
+  if( af == 6 ) {
+    s->pkt.ether_type = CI_ETHERTYPE_IP6;
+    hexbytes(raddr, (unsigned char*) s->pkt.ipx.ip6.daddr, 16);
+    s->pkt.ipx.ip6.next_hdr = (unsigned char) proto;
+  }
+  else {
+    unsigned char b[4];
+    s->pkt.ether_type = CI_ETHERTYPE_IP;
+    hexbytes(raddr, b, 4);
+    memcpy(&s->pkt.ipx.ip4.ip_daddr_be32, b, 4);
+    s->pkt.ipx.ip4.ip_protocol = (unsigned char) proto;
+  }
+  ipcache_lport_be16(&s->pkt) = (ci_uint16) lport;
+  ipcache_rport_be16(&s->pkt) = (ci_uint16) rport;
+  if( flags & 1 )
+    s->s_flags |= CI_SOCK_FLAG_CONNECTED;
+  if( flags & 2 ) {
+    s->rx_bind2dev_ifindex = 1;
+    s->rx_bind2dev_hwports = hwports;
+    s->rx_bind2dev_vlan = (ci_int16) vlan;
+  }
+  else {
+    s->rx_bind2dev_ifindex = CI_IFID_BAD;
+  }
+  /* Every receive queue has room: ci_udp_rx_deliver_to_future's recvq
+   * test (udp_internal.h:47-48) then depends on the tables alone. */
+  if( proto == IPPROTO_UDP )
+    SOCK_TO_UDP(s)->stats.max_recvq_pkts = 1u << 30;
+  printf("ok\n");
+}
+
+/* ---- one frame through handle_rx_csum_bad */
+static void do_frame(int intf, const char* hex)
+{
+  static ci_ip_pkt_fmt* pkt;
+  static struct ci_netif_poll_state ps;
+  int len = (int) strlen(hex) / 2, handled, i;
+  if( pkt == NULL )
+    pkt = aligned_alloc(4096, 64 * 1024);
+  memset(pkt, 0, sizeof(*pkt));
+  pkt->pkt_start_off = 0;
+  pkt->pkt_eth_payload_off = PKT_START_OFF_BAD;
+  pkt->frag_next = OO_PP_NULL;
+  pkt->refcount = 1 << 20;
+  pkt->intf_i = (ci_int16) intf;
+  if( len > 64 * 1024 - (int) CI_MEMBER_OFFSET(ci_ip_pkt_fmt, dma_start) - 64 ) {
+    printf("toolong\n");
+    return;
+  }
+  hexbytes(hex, (unsigned char*) PKT_START(pkt), len);
+  memset(&R, 0, sizeof(R));
+  for( i = 0; i < 3; ++i )
+    R.n[i] = R.first[i] = -1;
+  R.fut = -2;
+  handled = handle_rx_csum_bad(ni, &ps, pkt, len);
+  printf("r %d %d %d %d %d %d %d %d %d %d %d %u %d\n", handled, R.kernel, R.entry, R.l4off,
+         R.ip_paylen, R.n[0], R.first[0], R.n[1], R.first[1], R.n[2], R.first[2], R.hash,
+         R.fut);
+}
+
+int main(void)
+{
+  static char line[1 << 16];
+  char a[64], b[64];
+  while( fgets(line, sizeof(line), stdin) ) {
+    int af, id, proto, vlan, rc, intf;
+    unsigned lport, rport, flags;
+    unsigned long long hw;
+    switch( line[0] ) {
+    case 'I': {
+      int log4, log6, ns, nintf, hwp[CI_CFG_MAX_INTERFACES] = {0}, k, pos = 0, used;
+      if( sscanf(line + 1, "%d %d %d %d%n", &log4, &log6, &ns, &nintf, &pos) < 4 )
+        return 2;
+      for( k = 0; k < nintf && k < CI_CFG_MAX_INTERFACES; ++k ) {
+        if( sscanf(line + 1 + pos, "%d%n", &hwp[k], &used) < 1 )
+          return 2;
+        pos += used;
+      }
+      do_init(log4, log6, ns, nintf, hwp);
+      break;
+    }
+    case 'S':
+      if( sscanf(line + 1, "%d %d %d %u %u %63s %u %llu %d", &id, &af, &proto, &lport,
+                 &rport, a, &flags, &hw, &vlan) != 9 || id < 0 || id >= nsocks_ )
+        return 2;
+      do_sock(id, af, proto, lport, rport, a, flags, hw, vlan);
+      break;
+    case 'A': {
+      ci_addr_t l, r;
+      if( sscanf(line + 1, "%d %d %63s %u %63s %u %d", &af, &id, a, &lport, b, &rport,
+                 &proto) != 7 )
+        return 2;
+      l = addr_of(af, a);
+      r = addr_of(af, b);
+      rc = ci_netif_filter_insert(ni, OO_SP_FROM_INT(ni, id),
+                                  af == 6 ? AF_SPACE_FLAG_IP6 : AF_SPACE_FLAG_IP4,
+                                  l, lport, r, rport, proto);
+      printf("%d\n", rc);
+      break;
+    }
+    case 'P': {
+      char* hex = line + 1;
+      char* end;
+      intf = (int) strtol(hex, &end, 10);
+      while( *end == ' ' )
+        ++end;
+      end[strcspn(end, "\r\n")] = 0;
+      do_frame(intf, end);
+      break;
+    }
+    default:
+      break;
+    }
+    fflush(stdout);
+  }
+  return 0;
+}

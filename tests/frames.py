@@ -156,6 +156,13 @@ def edge_world():
     add(13, _sock(6, 443), 6, L6A, 443, None, 0, 6)                          # TCP6 listener
     add(14, _sock(17, 6002, raddr6=PEER6, rport=7777, flags=_abi.SOCK_CONNECTED), 6, L6A, 6002,
         PEER6, 7777, 17)
+    # an unconnected UDP socket beside the connected socket 2: a packet from
+    # PEER4:7002 matches socket 2 in stage 1 and this one in stage 2 (the
+    # future rule then gives up, udp_internal.h:41-52), others only this one
+    add(15, _sock(17, 5002), 4, L4A, 5002, None, 0, 17)
+    # a connected UDP socket alone on its port: its stage-1 match resolves
+    # the future
+    add(16, _sock(17, 5004, PEER4, 7004, flags=_abi.SOCK_CONNECTED), 4, L4A, 5004, PEER4, 7004, 17)
     return socks, filters
 
 
@@ -198,6 +205,8 @@ def edge_frames(seed: int = 1234) -> list[tuple[bytes, int]]:
         add(_u4(7002, 5002, pay(n)))
         add(_u4(33333, 5001, pay(n)))
         add(_u4(33333, 5999, pay(n)))
+        add(_u4(7003, 5002, pay(n)))
+        add(_u4(7004, 5004, pay(n)))
     add(_u4(1234, 5000, pay(30), dst=MC4, udst=MC4))
     add(eth(ipv4(PEER4, ip("255.255.255.255"), 17,
                  udp(4, PEER4, ip("255.255.255.255"), 1, 5001, pay(10))), 0x0800))

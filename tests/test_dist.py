@@ -234,3 +234,34 @@ def test_bench_rejects_gpus_world_mismatch():
     r = _bench(["--gpus", "4"], env)
     assert r.returncode != 0
     assert "WORLD_SIZE" in r.stderr
+
+
+def test_launcher_stops_all_ranks_when_one_dies(tmp_path):
+    """The rank launcher's watchdog: rank 1 of 3 dies while the other two
+    block (as they would in a barrier or an RCCL collective); the launcher
+    terminates them and returns rank 1's status within a bound, instead of
+    hanging until an outer timeout."""
+    import time
+    import bench
+    script = tmp_path / "rank.py"
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    script.write_text(
+        "import os, sys, time\n"
+        f"open(os.path.join({str(pids)!r}, os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+        "if os.environ['RANK'] == '1':\n"
+        "    time.sleep(0.5)\n"
+        "    sys.exit(7)\n"
+        "time.sleep(120)\n")
+    t = time.time()
+    rc = bench.launch_ranks(3, [], script=str(script), grace_s=5.0)
+    assert rc == 7
+    assert time.time() - t < 30
+    for r in ("0", "2"):  # the blocked ranks are gone
+        pid = int((pids / r).read_text())
+        try:
+            os.kill(pid, 0)
+            alive = os.path.exists(f"/proc/{pid}") and "Z" not in open(f"/proc/{pid}/stat").read().split()[2]
+        except ProcessLookupError:
+            alive = False
+        assert not alive, f"rank {r} still running"

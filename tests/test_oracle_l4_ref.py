@@ -1,0 +1,77 @@
+# SPDX-License-Identifier: BSD-2-Clause
+"""The oracle against the reference's own receive path (tests/l4_ref.py,
+tests/golden/ref_l4_golden.npz): for every frame of the edge corpora and of
+configuration samples 2-5, the gates, the L4 entry, each lookup stage's
+matches and socket, the pass-to-kernel decisions and the UDP / TCP future
+sockets the reference computed -- handle_rx_csum_bad, handle_rx_pkt,
+ci_udp_handle_rx, ci_tcp_handle_rx, ci_netif_filter_for_each_match and the
+pre-future helpers, compiled unmodified (oracle/ref_l4_harness.c).  When the
+harness binary is present (this container) the fixtures are also re-derived
+live."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import l4_ref
+from frames import pack
+from oracle_lib import OracleStack
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "ref_l4_golden.npz")
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_l4")
+
+
+def oracle_records(name):
+    socks, filters, hwports, frames = l4_ref.corpus(name)
+    o = OracleStack(intf_hwport=hwports)
+    for i, s in socks.items():
+        assert o.sock_set(i, s) == 0
+    for (i, af, la, lp, ra, rp, proto) in filters:
+        assert o.filter_insert_raw(i, af, la, lp, ra, rp, proto) == 0
+    buf, desc = pack(frames)
+    return o.handle_rx_batch(buf, desc, nthreads=4), frames
+
+
+@pytest.mark.parametrize("name", l4_ref.CORPORA)
+def test_oracle_matches_reference_run(name):
+    golden = np.load(GOLDEN)
+    out, sha = l4_ref.load(golden, name)
+    recs, frames = oracle_records(name)
+    assert l4_ref.frames_sha(frames) == sha, "the generator no longer makes the fixture's frames"
+    assert len(recs) == len(out)
+    bad = l4_ref.mismatches(recs, out)
+    assert not bad, "\n".join(bad)
+
+
+def test_fixture_covers_the_rules():
+    """The corpora reach every decision the fixture pins: all three TCP
+    stages, both UDP stages with multi-match, the UDP future given up by a
+    stage-2 match after a single stage-1 one, kernel hand-offs with and
+    without an L4 entry."""
+    golden = np.load(GOLDEN)
+    out = np.concatenate([l4_ref.load(golden, n)[0] for n in l4_ref.CORPORA])
+    c = {k: out[:, i] for i, k in enumerate(l4_ref.COLS)}
+    tcp, udp = c["entry"] == 6, c["entry"] == 17
+    assert ((c["n1"] > 0) & tcp).any() and ((c["n2"] > 0) & tcp).any() and \
+        ((c["n3"] > 0) & tcp).any()
+    assert ((c["n1"] > 0) & udp).any() and ((c["n2"] > 1) & udp).any()
+    assert ((c["n1"] == 1) & udp & (c["fut"] == -1)).any()   # given up: stage 2 matched too
+    assert ((c["n1"] == 1) & udp & (c["fut"] >= 0)).any()
+    assert ((c["kernel"] == 1) & (c["entry"] == 0)).any()
+    assert ((c["kernel"] == 1) & tcp & (c["n1"] < 0)).any()   # TCP scattered
+
+
+@pytest.mark.skipif(not os.path.exists(HARNESS), reason="oracle/_ref/ref_l4 is built only "
+                    "where /root/reference is (this container)")
+@pytest.mark.parametrize("name", ("edge", "c5"))
+def test_fixture_rederived_live(name):
+    socks, filters, hwports, frames = l4_ref.corpus(name)
+    lines = l4_ref.world_script(socks, filters, hwports) + \
+        [f"P {intf} {f.hex()}" for f, intf in frames]
+    p = subprocess.run([HARNESS], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                       check=True)
+    rows = np.array([list(map(int, x.split()[1:])) for x in p.stdout.splitlines()
+                     if x.startswith("r ")], dtype=np.int64)
+    np.testing.assert_array_equal(rows, l4_ref.load(np.load(GOLDEN), name)[0])

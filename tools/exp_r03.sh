@@ -60,6 +60,44 @@ a)  # baseline of the round: tests, store ablations, stamps, batch-size sweep
   step counters 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
   grep -i -E "utcl|tlb|translation" "$OUT/counters.txt" | head -40
   ;;
+b)  # tests, driver-shaped bench lines, kernel trace, TLB counters at 2^20 / 2^21
+  tests
+  for r in 1 2; do
+    step bench$r 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench$r.json" 2> "$OUT/bench$r.err"
+    cat "$OUT/bench$r.json"
+  done
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o run \
+     --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline \
+     > "$ROOT/$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -5 "$OUT/prof.log"; exit 1; }
+  find "$OUT/prof" -name "*kernel_stats.csv" -exec cat {} \;
+  for n in 1048576 2097152; do
+    for pass in "tlb1 TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_STALL_MULTI_MISS_sum" \
+                "tlb2 TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_UTCL1_SERIALIZATION_STALL_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"; do
+      set -- $pass; name=$1; shift
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d "$ROOT/$OUT/${name}_$n" \
+         -o run --output-format csv -- python3 "$ROOT/bench.py" --n $n --steps 5 --warmup 1 \
+         --no-cpu-baseline > "$ROOT/$OUT/${name}_$n.log" 2>&1) || { echo "pmc $name $n failed"; tail -3 "$OUT/${name}_$n.log"; exit 1; }
+    done
+  done
+  python3 -c "import sys, glob, os; sys.path.insert(0, 'tools'); from pmc_summary import counters; [print(d, counters(d)) for d in sorted(glob.glob('$OUT/tlb*_*')) if os.path.isdir(d)]" > "$OUT/tlb_summary.txt" 2>&1
+  cat "$OUT/tlb_summary.txt"
+  ;;
+c)  # steps / profiler sensitivity of the config-2 line; table maintenance timing
+  TESTS_K="table or poll or stream or l4" tests
+  for spec in "20 a" "50 a" "200 a" "20 b" "50 b"; do
+    set -- $spec
+    step s$1$2 300 python bench.py --steps $1 --warmup 5 --no-cpu-baseline > "$OUT/s$1$2.json" 2>/dev/null
+    echo "steps $1 ($2): $(python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); r=d["roofline"]; print(r["kernel_ms"], d["ms_per_step"], r["frac"])' "$OUT/s$1$2.json")"
+  done
+  for st in 20 50; do
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$ROOT/$OUT/prof$st" -o run \
+       --output-format csv -- python3 "$ROOT/bench.py" --steps $st --warmup 5 --no-cpu-baseline \
+       > "$ROOT/$OUT/prof$st.log" 2>&1) || { echo "rocprof failed"; tail -5 "$OUT/prof$st.log"; exit 1; }
+    echo "rocprof steps $st: $(grep -o '"kernel_ms": [0-9.]*' "$OUT/prof$st.log")"
+  done
+  step tableops 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --table-ops > "$OUT/tableops.json" 2> "$OUT/tableops.err"
+  grep -o '"table_ops": {[^}]*}' "$OUT/tableops.json"
+  ;;
 *)
   echo "unknown phase $PHASE"; exit 2 ;;
 esac
