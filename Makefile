@@ -23,7 +23,7 @@ CHECK_VARIANTS := r6e4:-DOO_RX_RING=6,-DOO_RX_EXTRA=4 r8e2:-DOO_RX_RING=8,-DOO_R
                   w1e0:-DOO_RX_WAVES=1,-DOO_RX_EXTRA=0
 CHECKS := $(foreach v,$(CHECK_VARIANTS),build/check/liboo_gpu_rx_$(firstword $(subst :, ,$(v))).so)
 
-all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling $(CHECKS)
+all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling tools/poll_bench $(CHECKS)
 
 build/check/liboo_gpu_rx_%.so: $(SRCS) $(HDRS)
 	@mkdir -p build/check
@@ -77,3 +77,10 @@ check-integration: oracle
 
 tools/hbm_ceiling: tools/hbm_ceiling.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
+
+# The deployed call shape of the batched RX branch: a C
+# caller of the shim, beside the oracle's per-event CPU loop.
+tools/poll_bench: tools/poll_bench.c $(SHIM) $(PKTGEN) oracle include/oo_rx_poll.h
+	$(CC) $(CFLAGS) -Iinclude -o $@ tools/poll_bench.c -Lonload_amd -l:liboo_rx_poll.so \
+	  -l:liboo_gpu_rx.so -l:liboo_pktgen.so -Loracle -l:liboorx_oracle.so \
+	  -Wl,-rpath,'$$ORIGIN/../onload_amd' -Wl,-rpath,'$$ORIGIN/../oracle'

@@ -254,6 +254,16 @@ int oo_gpu_rx_table_export(oo_gpu_rx_ctx* ctx, void* dst, uint64_t bytes, void* 
 int oo_gpu_rx_table_import(oo_gpu_rx_ctx* ctx, const void* src, uint64_t bytes,
                            void* stream);
 
+/* The mean frame length of the batches to come, in bytes (0, the default:
+ * infer it from the frame buffer's bytes per packet, right for packed
+ * batches but not for an AF_XDP UMEM of 2048-B chunks).  The transform
+ * compiles two instances of its kernel -- for frames under 1 KiB one that
+ * keeps more waves per CU, since short frames are bound by the per-packet
+ * header and lookup chain rather than the byte stream -- and
+ * picks one per batch by this.  Results are identical either way.
+ * 0 or -EINVAL. */
+int oo_gpu_rx_set_len_hint(oo_gpu_rx_ctx* ctx, uint32_t mean_frame_len);
+
 /* Device-resident batch: frames, descriptors and results all in HBM.
  * Enqueues the transform of n frames on `stream` and returns immediately.
  * d_counters (device, may be NULL) is incremented per reason.

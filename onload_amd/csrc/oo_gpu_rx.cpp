@@ -199,6 +199,7 @@ struct oo_gpu_rx_ctx {
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t grid_short = 0;     // resident blocks of the short-frame rx_kernel (0: unused)
   uint32_t kmode = 0;          // rx kernel: 0 by frame size, 1 always the 4-slot, 2 always the 2-slot
+  uint32_t len_hint = 0;       // mean frame length of the batches to come (0: from buffer bytes)
   uint32_t tstep = 8;          // tile size step (KParams::tstep)
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
   // host path
@@ -906,6 +907,12 @@ int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   return prepare(c, static_cast<hipStream_t>(stream));
 }
 
+int oo_gpu_rx_set_len_hint(oo_gpu_rx_ctx* c, uint32_t mean_frame_len) {
+  if (c == nullptr || mean_frame_len > 65535u) return -EINVAL;
+  c->len_hint = mean_frame_len;
+  return 0;
+}
+
 int oo_gpu_rx_stream_done(oo_gpu_rx_ctx* c, void* stream) {
   if (c == nullptr) return -EINVAL;
   if (!has_dev(c)) return 0;
@@ -1051,7 +1058,11 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // 2-slot-ring rx_kernel, whose smaller LDS footprint fits 12 waves per CU
   // instead of 10 (same-box A/B: config 3 -7 %, config 5 -2 %; config 2
   // +11 %, so long frames keep the 4-slot ring).
-  const bool short_frames = P.frames_bytes < 1024ull * n;
+  // By the caller's mean-frame-length hint when it gave one (a UMEM of
+  // 2048-B chunks says nothing about its frames), else by the buffer bytes
+  // per packet (a packed batch).
+  const bool short_frames =
+      c->len_hint ? c->len_hint < 1024u : P.frames_bytes < 1024ull * n;
   const bool use_short = !tx && c->grid_short > 0 && (c->kmode == 2 || (c->kmode == 0 && short_frames));
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full

@@ -165,6 +165,13 @@ class GpuRxStack:
         if rc:
             raise OSError(-rc, "oo_gpu_rx_sync_tables")
 
+    def set_len_hint(self, mean_frame_len: int) -> None:
+        """Mean frame length of the batches to come (0: inferred from the
+        buffer bytes per packet); picks the kernel instance."""
+        rc = self._lib.oo_gpu_rx_set_len_hint(self._ctx, int(mean_frame_len))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_set_len_hint")
+
     def stream_done(self, stream: int) -> None:
         """The caller is about to destroy `stream` (oo_gpu_rx_stream_done)."""
         rc = self._lib.oo_gpu_rx_stream_done(self._ctx, ctypes.c_void_p(stream))

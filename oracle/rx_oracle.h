@@ -37,9 +37,10 @@ int  oo_or_slot(const oo_or_tables* t, int af, uint32_t slot,
 int  oo_or_sock_set(oo_or_tables* t, int32_t id, const oo_gpu_rx_sock* s);
 uint32_t oo_or_dump(const oo_or_tables* t, int64_t* rows, uint32_t cap);
 
-/* One frame: the whole handle_rx_csum_bad -> handle_rx_pkt -> L4 demux. */
+/* One IPv4 lookup stage (ci_netif_filter_for_each_match): matches, first. */
 int  oo_or_walk4(const oo_or_tables* t, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
                  uint32_t proto, int intf_i, int vlan, int stop, int32_t* first);
+/* One frame: the whole handle_rx_csum_bad -> handle_rx_pkt -> L4 demux. */
 void oo_or_rx_one(const oo_or_tables* t, const uint8_t* frame, int len,
                   int intf_i, oo_gpu_rx_result* out);
 /* A batch over `nthreads` host threads (contiguous shards); a descriptor

@@ -97,6 +97,14 @@ c)  # steps / profiler sensitivity of the config-2 line; table maintenance timin
   done
   step tableops 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --table-ops > "$OUT/tableops.json" 2> "$OUT/tableops.err"
   grep -o '"table_ops": {[^}]*}' "$OUT/tableops.json"
+  for kv in "HIP_FORCE_DEV_KERNARG=1" "HIP_FORCE_DEV_KERNARG=0"; do
+    step kernarg 300 env $kv python bench.py --steps 50 --warmup 5 --no-cpu-baseline > "$OUT/ka.json" 2>/dev/null
+    echo "$kv: $(python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); r=d["roofline"]; print(r["kernel_ms"], d["ms_per_step"], r["frac"])' "$OUT/ka.json")"
+  done
+  step poll 300 tools/poll_bench 2 262144 64 1024 65536 > "$OUT/poll_c2.jsonl" 2> "$OUT/poll.err"
+  cat "$OUT/poll_c2.jsonl"
+  step poll3 300 tools/poll_bench 3 262144 64 1024 65536 > "$OUT/poll_c3.jsonl" 2>> "$OUT/poll.err"
+  cat "$OUT/poll_c3.jsonl"
   ;;
 *)
   echo "unknown phase $PHASE"; exit 2 ;;
