@@ -99,23 +99,26 @@ static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
 constexpr int NTRACK = 8;             // streams tracked at once (LRU)
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
-constexpr uint32_t CLAIM_SLOTS = NTRACK;  // tile-claim counter sets: one per tracked stream
-constexpr uint32_t CLAIM_GROUPS = 64; // wave groups per launch at most (128 B each)
+// Tile-claim counter sets: two per tracked stream (its launches alternate
+// between them), oo_rx::CLAIM_GROUPS counters of 128 B each.
+constexpr uint32_t CLAIM_SETS = 2 * NTRACK;
+using oo_rx::CLAIM_GROUPS;
 
 // One stream the context launches on.  Nothing is recorded per launch: a
 // table change (flush_ops) records `ev` on every other stream that launched
 // since the last change and makes its own stream wait for it, which orders
 // the change after every batch already enqueued there.  The entry's index
-// is also the stream's tile-claim counter set: launches on one stream run in
-// order, so the set is free whenever the stream's next launch starts; an
-// entry handed to another stream makes that stream wait for the old one
-// first (track_of).
+// also picks the stream's two tile-claim counter sets: launches on one stream
+// run in order and alternate between them, each zeroing the other as it
+// starts; an entry handed to another stream makes that stream wait for the
+// old one first (track_of).
 struct Tracked {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
   bool used = false;      // assigned to s
   bool live = false;      // launched on s since a table change last ordered itself after s
   bool gone = false;      // oo_gpu_rx_stream_done: ev already covers all of s's work
+  uint32_t parity = 0;    // claim set of the next launch (of the entry's two)
   uint32_t tables_seen = 0;  // table generation this stream has waited for
   uint64_t lru = 0;
 };
@@ -189,7 +192,7 @@ struct oo_gpu_rx_ctx {
   Tracked track[NTRACK];
   uint64_t lru = 0;
   uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros + the sink
-  uint32_t* d_claim = nullptr; // CLAIM_SLOTS x CLAIM_GROUPS counter pairs, 128 B apart
+  uint32_t* d_claim = nullptr; // CLAIM_SETS x CLAIM_GROUPS counters, 128 B apart
   bool failed = false;         // a table flush failed part-way: the device copy is unknown
   bool dyn = true;             // dynamic tile claims (OO_RX_STATIC=1: static)
   uint32_t tail_tile = 32;     // packets per tile at the batch's end (dynamic)
@@ -790,8 +793,8 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       hipMalloc(&T.socks, sizeof(oo_gpu_rx_sock) * c->max_socks) == hipSuccess &&
       hipMalloc(&T.sockgen, sizeof(uint32_t) * c->max_socks) == hipSuccess &&
       hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + 64u * 32u) == hipSuccess &&
-      hipMalloc(&c->d_claim, 128u * CLAIM_SLOTS * CLAIM_GROUPS) == hipSuccess &&
-      hipMemsetAsync(c->d_claim, 0, 128u * CLAIM_SLOTS * CLAIM_GROUPS, c->stream) == hipSuccess &&
+      hipMalloc(&c->d_claim, 128u * CLAIM_SETS * CLAIM_GROUPS) == hipSuccess &&
+      hipMemsetAsync(c->d_claim, 0, 128u * CLAIM_SETS * CLAIM_GROUPS, c->stream) == hipSuccess &&
       hipHostMalloc(&c->h_image_hdr, sizeof(ImageHdr), hipHostMallocDefault) == hipSuccess &&
       hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
       oo_table_launch_init(&T, c->stream) == 0;
@@ -1069,17 +1072,19 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   const uint32_t blocks = std::max<uint32_t>(
       1, std::min<uint32_t>((need + wpb - 1) / wpb, use_short ? c->grid_short : c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
-  // The launch's claim counters (zero: every launch leaves them reset), one
-  // pair per wave group: the largest power of two <= the group limit with
+  // The launch's claim counters (zeroed by the stream's previous launch),
+  // one per wave group: the largest power of two <= the group limit with
   // ngroups << gshift <= W (every group has a wave).  Short frames (under
   // 1 KiB of buffer per packet: header-bound tiles, many claims per us) use
   // 32 groups of eight-block runs, each group spread over all eight XCDs;
   // long frames 64 groups of single waves (same-box A/B).
-  // The stream's own claim counter set (Tracked): launches on one stream
-  // run in order, and every launch leaves its counters reset.
+  // The stream's own claim counter sets (Tracked): launches on one stream
+  // run in order and alternate between the two.
   Tracked* trk = track_of(c, s);
   if (trk == nullptr) return -EIO;
-  P.claim = c->d_claim + 32u * CLAIM_GROUPS * track_index(c, trk);
+  uint32_t* const sets = c->d_claim + 2u * 32u * CLAIM_GROUPS * track_index(c, trk);
+  P.claim = sets + 32u * CLAIM_GROUPS * trk->parity;
+  P.claim_next = sets + 32u * CLAIM_GROUPS * (trk->parity ^ 1u);
   uint32_t gmax = c->ngroups_max ? c->ngroups_max : (short_frames ? 32u : CLAIM_GROUPS);
   P.gshift = std::min<uint32_t>(c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u), 16u);
   while (P.gshift > 0 && (1ull << P.gshift) > W) --P.gshift;
@@ -1124,7 +1129,8 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   const int grid = (int)blocks;
   const int rc = tx ? oo_tx_launch(&P, grid, s)
                     : use_short ? oo_rx_launch_short(&P, grid, s) : oo_rx_launch(&P, grid, s);
-  if (rc != 0) return -EIO;
+  if (rc != 0) return -EIO;  // (nothing ran: the set stays zero for the next launch)
+  trk->parity ^= 1u;
   if (!tx) note_launch(trk);
   return 0;
 }

@@ -138,6 +138,10 @@ struct DevTables {
 // those reads spread over the L2 channels).
 constexpr uint32_t ZERO_LINES = 4096;
 
+// Wave groups of a launch at most: each has a tile-claim counter on a
+// 128-B line of its own (KParams::claim).
+constexpr uint32_t CLAIM_GROUPS = 64;
+
 // Kernel arguments (passed by value).
 struct KParams {
   const uint8_t* frames;
@@ -163,7 +167,8 @@ struct KParams {
   const uint8_t* zero;   // ZERO_LINES x 16 B of zeros (lanes with nothing to read)
   uint8_t* sink;         // 64 x 32 B written by lanes without a packet (rx_kernel)
   uint64_t* stamps;      // diagnostic builds (OO_RX_STAMPS) only; may be null
-  uint32_t* claim;       // per wave group, 128 B apart: {claims, finished waves}, 0 at launch
+  uint32_t* claim;       // one counter per wave group, 128 B apart, 0 at launch
+  uint32_t* claim_next;  // the set the stream's next launch claims from: zeroed here
   uint32_t ngroups;      // wave groups (a power of two, ngroups << gshift <= waves)
   uint32_t gshift;       // wave gwave is in group (gwave >> gshift) mod ngroups
   uint32_t dyn;          // 1: tiles past a wave's first three are claimed

@@ -10,6 +10,8 @@
   16-bit check-field stores (NST_TX), all global (a flat store counts in
   lgkmcnt too) -- a compiler that merged or split stores would make the
   waits too loose (round 1's byte stores were in fact merged).
+  Besides them each kernel has one 4-B `sc1` store, before its tile loop:
+  the next launch's claim counters zeroed (drained by the prologue's wait).
 
 Compiles the kernel source to assembly with hipcc (cross-compiles, no GPU)."""
 import os
@@ -78,11 +80,14 @@ def test_store_counts(asm):
     rx = _body(text, "_ZN5oo_rx9rx_kernelENS_7KParamsE")
     # store_records: two 16-B stores per tile (NST)
     assert len(re.findall(r"global_store_dwordx4", rx)) == 2
-    assert not re.findall(r"global_store_(byte|short|dword\b|dwordx2)", rx)
+    assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
+    assert len(re.findall(r"global_store_dword .* sc1$", rx, re.M)) == 1  # claim_next
+    assert len(re.findall(r"global_store_dword\b", rx)) == 1
     tx = _body(text, "_ZN5oo_rx9tx_kernelENS_7KParamsE")
     assert len(re.findall(r"global_store_short\b", tx)) == 2
     assert len(re.findall(r"global_store_dwordx4", tx)) == 4
-    assert not re.findall(r"global_store_(byte|dword\b|dwordx2)", tx)
+    assert not re.findall(r"global_store_(byte|dwordx2)", tx)
+    assert len(re.findall(r"global_store_dword\b", tx)) == 1
     for body in (rx, tx):  # flat stores would count in lgkmcnt as well
         assert not re.findall(r"flat_store|flat_load|flat_atomic", body)
 
@@ -95,5 +100,6 @@ def test_short_kernel_same_invariants(asm_short):
     rx = _body(text, RX_SHORT)
     assert "scratch_" not in rx
     assert len(re.findall(r"global_store_dwordx4", rx)) == 2
-    assert not re.findall(r"global_store_(byte|short|dword\b|dwordx2)", rx)
+    assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
+    assert len(re.findall(r"global_store_dword\b", rx)) == 1  # claim_next
     assert not re.findall(r"flat_store|flat_load|flat_atomic", rx)

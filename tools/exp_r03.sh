@@ -106,6 +106,19 @@ c)  # steps / profiler sensitivity of the config-2 line; table maintenance timin
   step poll3 300 tools/poll_bench 3 262144 64 1024 65536 > "$OUT/poll_c3.jsonl" 2>> "$OUT/poll.err"
   cat "$OUT/poll_c3.jsonl"
   ;;
+d)  # claim sets alternating per launch (no end-of-launch reset) vs HEAD; I-cache and VMEM level counters
+  TESTS_K="table or stream or claim or parity or wait_variants or dist" tests
+  ab 3 "2 3" onload_amd/liboo_gpu_rx.so build/var_ref.so
+  for pass in "ic SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+              "lv SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES"; do
+    set -- $pass; name=$1; shift
+    (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d "$ROOT/$OUT/$name" \
+       -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 \
+       --no-cpu-baseline > "$ROOT/$OUT/$name.log" 2>&1) || { echo "pmc $name failed"; tail -3 "$OUT/$name.log"; exit 1; }
+  done
+  python3 -c "import sys, glob, os; sys.path.insert(0, 'tools'); from pmc_summary import counters; [print(d, counters(d)) for d in sorted(glob.glob('$OUT/*')) if os.path.isdir(d)]" > "$OUT/pmc_summary.txt" 2>&1
+  cat "$OUT/pmc_summary.txt"
+  ;;
 *)
   echo "unknown phase $PHASE"; exit 2 ;;
 esac
