@@ -119,6 +119,11 @@ d)  # claim sets alternating per launch (no end-of-launch reset) vs HEAD; I-cach
   python3 -c "import sys, glob, os; sys.path.insert(0, 'tools'); from pmc_summary import counters; [print(d, counters(d)) for d in sorted(glob.glob('$OUT/*')) if os.path.isdir(d)]" > "$OUT/pmc_summary.txt" 2>&1
   cat "$OUT/pmc_summary.txt"
   ;;
+e)  # deep turns through the header rows: parity of the check builds, then depth A/B
+  TESTS_K="wait_variants or gpu_parity or l4_ref" tests
+  ab 3 "2 4" onload_amd/liboo_gpu_rx.so build/var_d8.so build/var_d16.so build/var_d32.so
+  ab 1 "3 5" onload_amd/liboo_gpu_rx.so build/var_d8.so build/var_d16.so
+  ;;
 *)
   echo "unknown phase $PHASE"; exit 2 ;;
 esac
