@@ -1858,27 +1858,6 @@ constexpr int NST = 2;
 constexpr int E = OO_RX_EXTRA;
 static_assert(E % 2 == 0 && E <= HC, "extra rounds live in the header rows");
 
-// Deep turns: a long tile keeps streaming through its header rows as well as
-// its ring (R + E rounds in flight instead of R) until about OO_RX_DEEP
-// rounds are left, and only then stages the next tile's header windows
-// there.  0: one such turn (the header rows go back to the windows as soon
-// as the extra rounds are read).
-#ifndef OO_RX_DEEP
-#define OO_RX_DEEP 0
-#endif
-// Turns of the R + E-row ring for an ext tile of T0 rounds (at least one;
-// the ring loop after them keeps >= OO_RX_DEEP rounds, or all of them past
-// the first turn).
-__device__ __forceinline__ uint32_t big_turns(uint32_t T0) {
-#if OO_RX_DEEP > 0
-  const uint32_t b = T0 > (uint32_t)OO_RX_DEEP ? (T0 - (uint32_t)OO_RX_DEEP) / (uint32_t)(R + E) : 0u;
-  return b > 1u ? b : 1u;
-#else
-  (void)T0;
-  return 1u;
-#endif
-}
-
 struct WaveLds {
   uint4 hdr[HC][64];            // header windows (stage_window)
   uint4 ring[R][64];            // body ring: slot = one round of the eight groups
@@ -2040,7 +2019,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     T0 = 0;
 #endif
     bool ext = E > 0 && T0 > (uint32_t)(R + E);
-    uint32_t T = ext ? (T0 - (R + E) * big_turns(T0) + R - 1) / R * R : (T0 + R - 1) / R * R;
+    uint32_t T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
     if (lane == 0) lds_write4(&L.T0, T0);
     IssueCursor ci;
     if (T0 != 0) issue_slot(ci, J, 0, lane, zero);  // (body-less tiles issue no rounds)
@@ -2098,8 +2077,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // rounds), and the claim of the tile after that.
     T0 = sreg(lds_read4(&L.T0));
     ext = E > 0 && T0 > (uint32_t)(R + E);
-    const uint32_t B = big_turns(T0);
-    T = ext ? (T0 - (R + E) * B + R - 1) / R * R : (T0 + R - 1) / R * R;
+    T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
     // Tile i + 2: the claim issued at the previous tile, read at its end
     // (have) or, after a tile without a body, here (the compiler waits for
     // it: vmcnt(0), which a body-less tile has little in flight to pay for).
@@ -2142,63 +2120,28 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // operations issued after the awaited pair (the demux loads excepted:
     // the demux waited for its last one, and with it for everything older).
     if (ext) {
-      // B turns of the R + E-row ring (ring rows, then header rows).  The
-      // first turn's rounds are 0..R+E-1; every turn refills the ring rows
-      // with the next turn's rounds, and all but the last the header rows
-      // too.  Each wait counts what is newer than the awaited pair: the rest
-      // of the turn's rounds, the refills so far, and in the first turn the
-      // descriptor line and the claim -- R + E (first turn) or R + E - 2 in
-      // all, until the last turn's header rows, which are not refilled.
-      auto turn = [&](auto first, auto last) {  // compile-time flags: static waits
-        constexpr int base = decltype(first)::value ? R + E : R + E - 2;
+      // Ring rounds 0..R-1, refilled with R+E..R+E+R-1: newer than the
+      // pair, the rest of the ring, the E header-row rounds, the descriptor
+      // line and the claim, and the refills so far -- R + E in all.
 #pragma unroll
-        for (int u = 0; u < R; u += 2) {
-          vm_wait<base>();
-          uint4 v0, v1;
-          lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
-          consume_round(cc, J, v0, lane);
-          consume_round(cc, J, v1, lane);
-          issue_round(ci, J, zero, &L.ring[u][0], lane);
-          issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
-        }
+      for (int u = 0; u < R; u += 2) {
+        vm_wait<R + E>();
+        uint4 v0, v1;
+        lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
+        issue_round(ci, J, zero, &L.ring[u][0], lane);
+        issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
+      }
+      // Header-row rounds R..R+E-1: newer, the rest of them, the descriptor
+      // line and the claim, and the R refills.
 #pragma unroll
-        for (int u = 0; u < E; u += 2) {
-          if constexpr (decltype(last)::value) vm_wait_n(base - u);
-          else vm_wait<base>();
-          uint4 v0, v1;
-          lds_read16x2(&L.hdr[u][lane], &L.hdr[u + 1][lane], v0, v1);
-          consume_round(cc, J, v0, lane);
-          consume_round(cc, J, v1, lane);
-          if constexpr (!decltype(last)::value) {
-            issue_round(ci, J, zero, &L.hdr[u][0], lane);
-            issue_round(ci, J, zero, &L.hdr[u + 1][0], lane);
-          }
-        }
-      };
-      using T_ = std::true_type;
-      using F_ = std::false_type;
-      if (B == 1) {
-        turn(T_{}, T_{});
-      } else {
-        // Turns 0..B-2, all R + E rows refilled: a rolled loop over the
-        // rows.  Each waits for R + E - 2 newer operations -- in the first
-        // turn that is two short of exact (the descriptor line and the
-        // claim are newer too), a stricter wait than needed, but the demux
-        // has drained the rounds before them.
-        for (uint32_t bt = 1; bt < B; ++bt) {
-#pragma unroll 1
-          for (int k = 0; k < R + E; k += 2) {
-            vm_wait<R + E - 2>();
-            uint4(*const rows)[64] = k < R ? &L.ring[k] : &L.hdr[k - R];
-            uint4 v0, v1;
-            lds_read16x2(&rows[0][lane], &rows[1][lane], v0, v1);
-            consume_round(cc, J, v0, lane);
-            consume_round(cc, J, v1, lane);
-            issue_round(ci, J, zero, &rows[0][0], lane);
-            issue_round(ci, J, zero, &rows[1][0], lane);
-          }
-        }
-        turn(F_{}, T_{});
+      for (int u = 0; u < E; u += 2) {
+        vm_wait_n(R + E - u);
+        uint4 v0, v1;
+        lds_read16x2(&L.hdr[u][lane], &L.hdr[u + 1][lane], v0, v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
       }
       stage_next();
     }

@@ -6,8 +6,7 @@ rx_kernel / tx_kernel wait for their LDS-DMA rounds with counted
 header-row rounds E, the staging operations per tile and the stores per tile
 (oo_rx_kernel.hip).  `make` also builds the same sources with other values
 (build/check/, Makefile CHECK_VARIANTS: R 6 / E 4, R 8 / E 2, one wave per
-block with E 0, deep turns through the header rows with R 4 / E 8 and
-R 6 / E 4); each build is loaded beside the product (its own soname) and
+block with E 0); each build is loaded beside the product (its own soname) and
 must stay bit-exact with the oracle -- a count that does not follow its
 constants shows up here as wrong sums, not only when the product's values
 change."""
@@ -25,7 +24,7 @@ from onload_amd.rx import GpuRxStack
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = ("r6e4", "r8e2", "w1e0", "d8", "r6e4d6")
+VARIANTS = ("r6e4", "r8e2", "w1e0")
 HWPORTS = (0, 1, 3, 2, 5)
 _libs: dict = {}
 

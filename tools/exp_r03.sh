@@ -124,6 +124,40 @@ e)  # deep turns through the header rows: parity of the check builds, then depth
   ab 3 "2 4" onload_amd/liboo_gpu_rx.so build/var_d8.so build/var_d16.so build/var_d32.so
   ab 1 "3 5" onload_amd/liboo_gpu_rx.so build/var_d8.so build/var_d16.so
   ;;
+f)  # fewer bytes in flight: smaller grids, fewer extra rounds (config 2)
+  L=onload_amd/liboo_gpu_rx.so
+  ab 3 2 $L $L@OO_RX_GRID_PCT=80 $L@OO_RX_GRID_PCT=90 $L@OO_RX_GRID_PCT=60 build/var_e4.so build/var_e6.so
+  ;;
+g)  # AF_XDP ring path in the 2048-B UMEM layout for the short-frame configs, with and without the length hint
+  for c in 3 5 2; do
+    step xdp$c 600 python bench.py --config $c --xdp --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/xdp_c$c.json" 2> "$OUT/xdp_c$c.err"
+    python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); r=d["roofline"]; print("c", sys.argv[2], "packed", r["kernel_ms"], r["frac"], "xdp", json.dumps(d["xdp_ring"]))' "$OUT/xdp_c$c.json" $c
+  done
+  ;;
+h)  # the launch's end in the stamps (config 2); HBM bytes of config 3 on the AF_XDP ring path
+  step stamps 300 env OO_RX_LIB=build/var_st.so python tools/stamps.py --config 2 > "$OUT/stamps_c2.json" 2> "$OUT/stamps.err"
+  cat "$OUT/stamps_c2.json"
+  for pass in "fetch FETCH_SIZE" "write WRITE_SIZE"; do
+    set -- $pass; name=$1; shift
+    (cd /tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc "$@" -d "$ROOT/$OUT/xdp3_$name" \
+       -o run --output-format csv -- python3 "$ROOT/bench.py" --config 3 --xdp --steps 5 --warmup 1 \
+       --no-cpu-baseline > "$ROOT/$OUT/xdp3_$name.log" 2>&1) || { echo "pmc $name failed"; tail -3 "$OUT/xdp3_$name.log"; exit 1; }
+  done
+  ;;
+i)  # deep turns for each wave's last tile (product) vs none (dl0)
+  TESTS_K="wait_variants or gpu_parity or l4_ref or tx or xdp" tests
+  ab 3 2 onload_amd/liboo_gpu_rx.so build/var_dl0.so
+  ab 1 "3 4 5" onload_amd/liboo_gpu_rx.so build/var_dl0.so
+  ;;
+j)  # deep-last on config 2 with more reps; deep-all + deep-last on config 4
+  ab 5 2 onload_amd/liboo_gpu_rx.so build/var_dl0.so
+  ab 2 4 onload_amd/liboo_gpu_rx.so build/var_d8dl.so build/var_d32dl.so build/var_dl0.so
+  ;;
+k)  # deep turns only for tiles longer than a threshold (config 4's jumbo tiles)
+  ab 3 4 onload_amd/liboo_gpu_rx.so build/var_t100.so build/var_t200.so build/var_t400.so build/var_d8dl.so
+  ab 2 2 onload_amd/liboo_gpu_rx.so build/var_t100.so build/var_t200.so
+  ab 1 5 onload_amd/liboo_gpu_rx.so build/var_t100.so build/var_t200.so
+  ;;
 *)
   echo "unknown phase $PHASE"; exit 2 ;;
 esac

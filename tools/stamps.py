@@ -129,6 +129,20 @@ def main() -> None:
                                 "first_12us": [round(float(x), 2) for x in frac[:12]],
                                 "p10_p90": [float(np.percentile(frac[5:-40], 10)),
                                             float(np.percentile(frac[5:-40], 90))] if span > 60 else None}
+    # The launch's end: live and streaming waves and the body bytes streamed
+    # (each tile's rounds x 1 KiB spread evenly over its stream phase), in
+    # 2-us bins over the last 40 us, against the mean rate of the middle.
+    kb = np.zeros(len(bins) - 1)
+    for w in range(waves):
+        for i in range(int(used[w].sum())):
+            t = (a[w, i, :6] - t0) * ns / 1e3
+            kb += np.histogram(np.linspace(t[3], t[4], 64), bins)[0] * (float(a[w, i, 7]) / 64)
+    if span > 60:
+        tail = slice(span - 40, span)
+        pair = lambda x: [round(float(x[tail][j:j + 2].sum() / 2), 2) for j in range(0, 40, 2)]  # noqa: E731
+        res["end_40us"] = {"live_waves": pair(live), "streaming_waves": pair(strm),
+                           "body_GBps": [round(v * 1.024, 0) for v in pair(kb)],
+                           "body_GBps_mid_mean": round(float(kb[20:span - 40].mean()) * 1.024, 0)}
     res["per_tile_k_us"] = {str(k): [round(float(np.mean((a[used[:, k], k, j + 1] - a[used[:, k], k, j]) * ns / 1e3)), 2)
                                      for j in range(5)]
                             for k in range(min(int(used.sum(1).max()), 8)) if used[:, k].any()}
