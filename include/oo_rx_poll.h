@@ -57,7 +57,11 @@
  * dispatch).  With OO_RX_POLL_ZERO_COPY the packet-buffer pool is
  * registered with the device at open and each frame is read where the NIC
  * put it (over PCIe, no host copy); otherwise the frames of a batch are
- * gathered into a registered buffer first.
+ * gathered into a registered buffer first.  In place, the buffer bytes per
+ * packet say nothing of the frames, so each batch sets the context's
+ * mean-frame-length hint (oo_gpu_rx_set_len_hint) to the batch's mean for
+ * its launch and clears it after: a context shared with other callers
+ * should not rely on a hint of its own while a zero-copy poll runs.
  */
 #ifndef OO_RX_POLL_H
 #define OO_RX_POLL_H

@@ -339,7 +339,7 @@ static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs
                         const oo_rx_poll_stats* base)
 {
   uint32_t i, m = 0;
-  uint64_t at = 0;
+  uint64_t at = 0, total = 0;
   int rc;
   c->evs = evs;
   c->n = n;
@@ -365,15 +365,22 @@ static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs
       d->len = e->len;
       d->intf_i = e->intf_i;
       d->rsvd = 0;
+      total += e->len;
       c->ev_of[m++] = i;
     }
   }
   c->m = m;
   if( m == 0 )
     return 0;
-  if( p->zero_copy )
+  if( p->zero_copy ) {
+    /* The frames sit in their 2048-B packet buffers, so the buffer bytes per
+     * packet say nothing of their length: the poll's mean length picks the
+     * kernel instance for this launch (and is cleared after it). */
+    (void)oo_gpu_rx_set_len_hint(p->gpu, (uint32_t)(total / m) ? (uint32_t)(total / m) : 1u);
     rc = oo_gpu_rx_submit_mapped(p->gpu, p->d_pool, p->cfg.pkt_bufs_bytes, c->d_desc, m,
                                  c->d_rec, &c->ticket);
+    (void)oo_gpu_rx_set_len_hint(p->gpu, 0);
+  }
   else if( p->mapped )
     rc = oo_gpu_rx_submit_mapped(p->gpu, c->d_pack, at, c->d_desc, m, c->d_rec, &c->ticket);
   else

@@ -158,6 +158,22 @@ k)  # deep turns only for tiles longer than a threshold (config 4's jumbo tiles)
   ab 2 2 onload_amd/liboo_gpu_rx.so build/var_t100.so build/var_t200.so
   ab 1 5 onload_amd/liboo_gpu_rx.so build/var_t100.so build/var_t200.so
   ;;
+l)  # a wave's last long tile through one R + E-row ring (product) vs not (w0)
+  TESTS_K="wait_variants or gpu_parity or l4_ref or tx or xdp or table" tests
+  ab 5 2 onload_amd/liboo_gpu_rx.so build/var_w0.so
+  ab 1 "3 4 5" onload_amd/liboo_gpu_rx.so build/var_w0.so
+  ;;
+m)  # config 2: claim groups spanning XCDs (runs of 2^gshift waves = 2^(gshift-1) blocks)
+  L=onload_amd/liboo_gpu_rx.so
+  ab 3 2 $L $L@OO_RX_GSHIFT=2 $L@OO_RX_GSHIFT=3 $L@OO_RX_GSHIFT=4 $L@OO_RX_GSHIFT=4,OO_RX_GROUPS=32
+  ;;
+n)  # bench lines and PMC passes (FETCH/WRITE/SQ/TCC) of configs 2-5 on the current kernel
+  for c in ${CONFIGS:-2 3 4 5}; do
+    step bench$c 300 python bench.py --config $c --steps 20 --warmup 5 > "$OUT/bench_c$c.json" 2> "$OUT/bench_c$c.err"
+    python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); r=d["roofline"]; print(sys.argv[1], r["kernel_ms"], r["frac"], d["value"])' "$OUT/bench_c$c.json"
+    CONFIG=$c CEILING=0 STEPS=5 bash tools/pmc.sh > "$OUT/pmc_c$c.log" 2>&1 || { echo "pmc c$c failed"; tail -5 "$OUT/pmc_c$c.log"; exit 1; }
+  done
+  ;;
 *)
   echo "unknown phase $PHASE"; exit 2 ;;
 esac
