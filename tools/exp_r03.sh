@@ -174,6 +174,28 @@ n)  # bench lines and PMC passes (FETCH/WRITE/SQ/TCC) of configs 2-5 on the curr
     CONFIG=$c CEILING=0 STEPS=5 bash tools/pmc.sh > "$OUT/pmc_c$c.log" 2>&1 || { echo "pmc c$c failed"; tail -5 "$OUT/pmc_c$c.log"; exit 1; }
   done
   ;;
+o)  # split tail tiles (last part to finish combines) vs whole tail tiles (OO_RX_SPLIT=0) vs HEAD
+  tests
+  L=onload_amd/liboo_gpu_rx.so
+  ab 5 2 $L $L@OO_RX_SPLIT=0 build/var_ref.so
+  ab 2 4 $L $L@OO_RX_SPLIT=0 build/var_ref.so
+  ab 1 "3 5" $L build/var_ref.so
+  ;;
+final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
+  tests
+  for r in 1 2; do
+    step bench$r 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench_c2_$r.json" 2> "$OUT/bench_c2_$r.err"
+    cat "$OUT/bench_c2_$r.json"
+  done
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o run \
+     --output-format csv -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 \
+     > "$ROOT/$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -5 "$OUT/prof.log"; exit 1; }
+  find "$OUT/prof" -name "*kernel_stats.csv" -exec cat {} \;
+  for c in 3 4 5; do
+    step bench_c$c 300 python bench.py --config $c --steps 20 --warmup 5 > "$OUT/bench_c$c.json" 2> "$OUT/bench_c$c.err"
+    python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); r=d["roofline"]; print(sys.argv[1], r["kernel_ms"], r["frac"], d["value"])' "$OUT/bench_c$c.json"
+  done
+  ;;
 *)
   echo "unknown phase $PHASE"; exit 2 ;;
 esac
