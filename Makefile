@@ -23,7 +23,7 @@ CHECK_VARIANTS := r6e4:-DOO_RX_RING=6,-DOO_RX_EXTRA=4 r8e2:-DOO_RX_RING=8,-DOO_R
                   w1e0:-DOO_RX_WAVES=1,-DOO_RX_EXTRA=0
 CHECKS := $(foreach v,$(CHECK_VARIANTS),build/check/liboo_gpu_rx_$(firstword $(subst :, ,$(v))).so)
 
-all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling tools/poll_bench $(CHECKS)
+all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling tools/ring_probe tools/poll_bench $(CHECKS)
 
 build/check/liboo_gpu_rx_%.so: $(SRCS) $(HDRS)
 	@mkdir -p build/check
@@ -76,6 +76,9 @@ check-integration: oracle
 .PHONY: all oracle asm clean variants check-integration
 
 tools/hbm_ceiling: tools/hbm_ceiling.hip
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
+
+tools/ring_probe: tools/ring_probe.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
 
 # The deployed call shape of the batched RX branch: a C

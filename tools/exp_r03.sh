@@ -181,6 +181,27 @@ o)  # split tail tiles (last part to finish combines) vs whole tail tiles (OO_RX
   ab 2 4 $L $L@OO_RX_SPLIT=0 build/var_ref.so
   ab 1 "3 5" $L build/var_ref.so
   ;;
+p)  # HEAD check after the restart; write-cost and half-line (sector) probes
+  tests
+  for r in 1 2; do
+    step bench$r 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench$r.json" 2> "$OUT/bench$r.err"
+    cat "$OUT/bench$r.json"
+  done
+  step probe 600 tools/ring_probe 1610612736 w > "$OUT/wr_probe.jsonl" 2> "$OUT/wr_probe.err"
+  cat "$OUT/wr_probe.jsonl"
+  step counters 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
+  grep -o -E "TCC_EA0?_RDREQ[A-Z0-9_]*|TCC_BUBBLE[A-Z0-9_]*|TCC_EA0?_WRREQ[A-Z0-9_]*" "$OUT/counters.txt" | sort -u | tr '\n' ' '; echo
+  for v in h0 h1; do
+    for pass in "fetch FETCH_SIZE" "rq TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+      set -- $pass; name=$1; shift
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d "$ROOT/$OUT/${v}_$name" \
+         -o run --output-format csv -- "$ROOT/tools/ring_probe" 1610612736 $v \
+         > "$ROOT/$OUT/${v}_$name.log" 2>&1) || { echo "pmc $v $name failed"; tail -3 "$OUT/${v}_$name.log"; }
+    done
+  done
+  python3 -c "import sys, glob, os; sys.path.insert(0, 'tools'); from pmc_summary import counters; [print(d, counters(d, 'ring_split')) for d in sorted(glob.glob('$OUT/h*_*')) if os.path.isdir(d)]" > "$OUT/sector_summary.txt" 2>&1
+  cat "$OUT/sector_summary.txt"
+  ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
   for r in 1 2; do

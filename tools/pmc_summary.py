@@ -22,12 +22,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def counters(path: str) -> dict:
+def counters(path: str, kernel: str = "rx_kernel") -> dict:
     files = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
     vals: dict = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if "rx_kernel" not in r["Kernel_Name"]:
+            if kernel not in r["Kernel_Name"]:
                 continue
             key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), r["Counter_Name"])
             vals.setdefault(r["Counter_Name"], {}).setdefault(key[0], 0.0)

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64) void ring_grp(const u32x4* __restrict__ p, size
 // instructions of eight frames x 128 B, as rx_kernel stages header windows),
 // then the other FB/128 - 1 lines of each frame by 8-lane groups.  HDRLAG:
 // the line-0 reads are for the NEXT tile (as rx_kernel's pipelined staging).
-template <int R, bool HDRLAG, int ST = 0>
+template <int R, bool HDRLAG, int ST = 0, int HAUX = 0, int SEC = 0>
 __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, size_t nframes,
                                                  uint32_t* out) {
   constexpr uint32_t fb16 = 96, lines = 12;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
         const size_t frame = th * 64 + i * 8 + g;
         __builtin_amdgcn_global_load_lds((const void*)(p + frame * fb16 + j),
                                          (void __attribute__((address_space(3)))*)(lds + (R + i) * 64),
-                                         16, 0, 0);
+                                         16, 0, HAUX);
       }
     }
     const uint32_t total = 8 * (lines - 1);  // rounds: 8 frames per group x 11 lines
@@ -176,7 +176,10 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
         wait_vm<R - 1>();
         const u32x4 v = lds[u * 64 + lane];
         acc = dot(v.x, dot(v.y, dot(v.z, dot(v.w, acc))));
-        __builtin_amdgcn_global_load_lds((const void*)src(k0 + R + u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
+        if (SEC == 0 || j < 4)  // SEC: only the lower half of every body line is read
+          __builtin_amdgcn_global_load_lds((const void*)src(k0 + R + u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
+        else
+          __builtin_amdgcn_global_load_lds((const void*)(src(k0 + R + u) - 4), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
       }
     }
     wait_vm<0>();
@@ -200,6 +203,10 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
       } else if (ST == 5) {
         asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\tglobal_store_dwordx4 %0, %1, off offset:16 nt sc1"
                      ::"v"(rec), "v"(r0) : "memory");
+      } else if (ST == 7) {  // two lanes per record: each instruction writes 1 KiB of whole lines
+        u32x4* rq = reinterpret_cast<u32x4*>(out) + 16 + t * 128 + lane;
+        rq[0] = r0;
+        rq[64] = r0;
       } else if ((t / gridDim.x) % 4 == 3) {  // 6: four tiles' records at once (8 KB)
         for (int q = 0; q < 4; ++q) {
           u32x4* rq = reinterpret_cast<u32x4*>(out) + 16 + ((t - q * gridDim.x) * 64 + lane) * 2;
@@ -212,8 +219,8 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
   if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <int R, bool HDRLAG, int ST = 0>
-static void run_split(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
+template <int R, bool HDRLAG, int ST = 0, int HAUX = 0, int SEC = 0>
+static void run_split(const u32x4* a, size_t bytes, uint32_t* o, int cu, const char* tag = "") {
   const size_t lds = (size_t)(R + 8) * 1024;
   const size_t nframes = (bytes - 4096) / 1536 / 64 * 64;
   for (int m : {8, 10}) {
@@ -224,15 +231,15 @@ static void run_split(const u32x4* a, size_t bytes, uint32_t* o, int cu) {
     float best = 1e9f;
     for (int r = 0; r < 10; ++r) {
       (void)hipEventRecord(e0, 0);
-      hipLaunchKernelGGL((ring_split<R, HDRLAG, ST>), dim3(grid), dim3(64), lds, 0, a, nframes, o);
+      hipLaunchKernelGGL((ring_split<R, HDRLAG, ST, HAUX, SEC>), dim3(grid), dim3(64), lds, 0, a, nframes, o);
       (void)hipEventRecord(e1, 0);
       (void)hipEventSynchronize(e1);
       float ms;
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (r >= 2 && ms < best) best = ms;
     }
-    printf("{\"split_hdr\":1,\"hdr_lag\":%d,\"stores\":%d,\"slots\":%d,\"waves_per_cu\":%d,\"GBps\":%.1f}\n",
-           (int)HDRLAG, ST, R, m, nframes * 1536 / (best * 1e-3) / 1e9);
+    printf("{\"split_hdr\":1,\"tag\":\"%s\",\"hdr_aux\":%d,\"half_lines\":%d,\"hdr_lag\":%d,\"stores\":%d,\"slots\":%d,\"waves_per_cu\":%d,\"ms\":%.4f,\"GBps\":%.1f}\n",
+           tag, HAUX, SEC, (int)HDRLAG, ST, R, m, best, nframes * 1536 / (best * 1e-3) / 1e9);
   }
 }
 
@@ -277,6 +284,29 @@ int main(int argc, char** argv) {
     run<8, 1>(a, bytes, o, cu);
     run<16, 1>(a, bytes, o, cu);
     run<32, 1>(a, bytes, o, cu);
+  }
+  if (argc > 2 && argv[2][0] == 'w') {  // write-cost and sector experiments (round 3)
+    uint32_t *uc = nullptr, *fg = nullptr;
+    const size_t ob = bytes / 40 + 4096;
+    if (hipExtMallocWithFlags((void**)&uc, ob, hipDeviceMallocUncached) != hipSuccess) uc = nullptr;
+    if (hipExtMallocWithFlags((void**)&fg, ob, hipDeviceMallocFinegrained) != hipSuccess) fg = nullptr;
+    for (int rep = 0; rep < 2; ++rep) {
+      run_split<4, true, 0>(a, bytes, o, cu, "reads");
+      run_split<4, true, 1>(a, bytes, o, cu, "records");
+      run_split<4, true, 7>(a, bytes, o, cu, "records_1k_per_instr");
+      run_split<4, true, 0, 2>(a, bytes, o, cu, "reads_all_nt");
+      run_split<4, true, 1, 2>(a, bytes, o, cu, "records_all_nt");
+      run_split<4, true, 7, 2>(a, bytes, o, cu, "records_1k_all_nt");
+      if (uc) run_split<4, true, 1>(a, bytes, uc, cu, "records_uncached_mem");
+      if (fg) run_split<4, true, 1>(a, bytes, fg, cu, "records_finegrained_mem");
+      run_split<4, true, 0, 0, 1>(a, bytes, o, cu, "reads_half_body_lines");
+    }
+    return 0;
+  }
+  if (argc > 2 && argv[2][0] == 'h') {  // one variant per run, for rocprofv3 --pmc
+    if (argv[2][1] == '1') run_split<4, true, 0, 0, 1>(a, bytes, o, cu, "reads_half_body_lines");
+    else run_split<4, true, 0>(a, bytes, o, cu, "reads");
+    return 0;
   }
   run_split<4, true>(a, bytes, o, cu);
   run_split<4, true, 1>(a, bytes, o, cu);
