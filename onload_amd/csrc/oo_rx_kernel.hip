@@ -69,6 +69,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef OO_RX_RING
 #define OO_RX_RING 4  // rx_kernel: body ring slots per wave (even)
 #endif
+#ifndef OO_RX_PF
+#define OO_RX_PF 0  // lines per frame requested up front for a wave's last tile (0: none)
+#endif
+#ifndef OO_RX_PF_LATE
+#define OO_RX_PF_LATE 0  // 1: those requests follow the demux instead of preceding the ring
+#endif
 
 constexpr int WAVES = OO_RX_WAVES;
 constexpr int R = OO_RX_RING;
@@ -1865,6 +1871,9 @@ struct WaveLds {
   uint32_t cnt[OO_RX_R_COUNT];  // per-reason counts
   uint32_t dbase, gofs;          // claims: first dynamic tile of the group, counter offset
   uint32_t T0, pad;              // the tile's body rounds (kept out of the registers)
+#if OO_RX_PF
+  uint32_t pf[64];               // landing place of the last tile's line requests (unread)
+#endif
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
 constexpr int WAVE_U4 = (int)(sizeof(WaveLds) / 16);
@@ -2023,12 +2032,35 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     if (lane == 0) lds_write4(&L.T0, T0);
     IssueCursor ci;
     if (T0 != 0) issue_slot(ci, J, 0, lane, zero);  // (body-less tiles issue no rounds)
+#if OO_RX_PF && !OO_RX_PF_LATE
+    // The wave's last tile: every line of its frames' bodies (at most
+    // OO_RX_PF per frame) is requested up front by 4-B LDS-DMA requests of the
+    // default policy, which leave the lines in L2 and the Infinity Cache; the
+    // ring below then reads them from there.  The launch ends with waves
+    // streaming their last tiles while others have finished: their ring
+    // depth, not HBM, bounds that stretch.
+    uint32_t npf = 0;
+    if (!TX && T0 != 0 && tnext >= P.ntiles) {
+      const uint32_t off0 = body_off0(dv.abase);
+      const uint32_t nl = dv.span > HB ? ((uint32_t)dv.span - off0 + 127u) >> 7 : 0u;
+      npf = min(wave_max(nl, lane), (uint32_t)OO_RX_PF);
+      const uint64_t a0 = dv.abase + off0;
+      for (uint32_t k = 0; k < npf; ++k) {
+        const uint64_t a = nl != 0 ? a0 + 128u * min(k, nl - 1u) : zero;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(a), (lptr)(&L.pf[0]), 4, 0, 0);
+      }
+    }
+#else
+    constexpr uint32_t npf = 0;
+#endif
     // This tile's header windows: older than the previous tile's NST stores
-    // (none before the first tile) and the R rounds issued here.
+    // (none before the first tile), the last tile's line requests and the R
+    // rounds issued here.
     if (T != 0) {
 #pragma unroll
       for (int u = 0; u < R; ++u) issue_round(ci, J, zero, &L.ring[u][0], lane);
-      if (it_ == 0) vm_wait<R>();
+      if (npf != 0) vm_wait_n((it_ == 0 ? R : R + NSTK) + (int)npf);
+      else if (it_ == 0) vm_wait<R>();
       else vm_wait<R + NSTK>();
     } else {
       if (it_ == 0) vm_wait<0>();
@@ -2078,6 +2110,22 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     T0 = sreg(lds_read4(&L.T0));
     ext = E > 0 && T0 > (uint32_t)(R + E);
     T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
+#if OO_RX_PF && OO_RX_PF_LATE
+    // (late form: the demux's loads are not queued behind these requests)
+    uint32_t npl = 0;
+    if (!TX && T0 != 0 && tnext >= P.ntiles) {
+      const uint32_t off0 = body_off0(dv.abase);
+      const uint32_t nl = dv.span > HB ? ((uint32_t)dv.span - off0 + 127u) >> 7 : 0u;
+      npl = min(wave_max(nl, lane), (uint32_t)min(OO_RX_PF, 16));
+      const uint64_t a0 = dv.abase + off0;
+      for (uint32_t k = 0; k < npl; ++k) {
+        const uint64_t a = nl != 0 ? a0 + 128u * min(k, nl - 1u) : zero;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(a), (lptr)(&L.pf[0]), 4, 0, 0);
+      }
+    }
+#else
+    constexpr uint32_t npl = 0;
+#endif
     // Tile i + 2: the claim issued at the previous tile, read at its end
     // (have) or, after a tile without a body, here (the compiler waits for
     // it: vmcnt(0), which a body-less tile has little in flight to pay for).
@@ -2125,7 +2173,8 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       // line and the claim, and the refills so far -- R + E in all.
 #pragma unroll
       for (int u = 0; u < R; u += 2) {
-        vm_wait<R + E>();
+        if (npl != 0) vm_wait_n(R + E + (int)npl);
+        else vm_wait<R + E>();
         uint4 v0, v1;
         lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
         consume_round(cc, J, v0, lane);
@@ -2137,7 +2186,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       // line and the claim, and the R refills.
 #pragma unroll
       for (int u = 0; u < E; u += 2) {
-        vm_wait_n(R + E - u);
+        vm_wait_n(R + E - u + (int)npl);
         uint4 v0, v1;
         lds_read16x2(&L.hdr[u][lane], &L.hdr[u + 1][lane], v0, v1);
         consume_round(cc, J, v0, lane);
@@ -2148,7 +2197,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // The ring loop (T is a multiple of R).  Newer than the awaited pair: the
     // rest of the ring, plus in the first turn the staging operations issued
     // since the ring was filled (NHS, or HC after an ext prefix); none past T.
-    const int nhs = ext ? HC : NHS;
+    const int nhs = ext ? HC : NHS + (int)npl;
     for (uint32_t k0 = 0; k0 < T; k0 += R) {
       const bool first = k0 == 0, last = k0 + R == T;
 #pragma unroll

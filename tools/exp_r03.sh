@@ -201,6 +201,16 @@ p)  # HEAD check after the restart; write-cost and half-line (sector) probes
   done
   python3 -c "import sys, glob, os; sys.path.insert(0, 'tools'); from pmc_summary import counters; [print(d, counters(d, 'ring_split')) for d in sorted(glob.glob('$OUT/h*_*')) if os.path.isdir(d)]" > "$OUT/sector_summary.txt" 2>&1
   cat "$OUT/sector_summary.txt"
+  # per-launch clock: GRBM_GUI_ACTIVE cycles per dispatch over 50 launches
+  (cd /tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d "$ROOT/$OUT/clk" \
+     -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline \
+     > "$ROOT/$OUT/clk.log" 2>&1) || { echo "pmc clk failed"; tail -3 "$OUT/clk.log"; }
+  # the wave's last tile requested up front (OO_RX_PF lines per frame)
+  OO_RX_LIB=build/var_pf16.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q \
+    -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pf_parity.log" 2>&1
+  rc=$?; tail -2 "$OUT/pf_parity.log"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  ab 3 2 onload_amd/liboo_gpu_rx.so build/var_pf16.so build/var_pf64.so build/var_pfl16.so
+  ab 1 "4 5" onload_amd/liboo_gpu_rx.so build/var_pf16.so
   ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
