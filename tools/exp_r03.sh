@@ -188,11 +188,12 @@ p)  # HEAD check after the restart; write-cost and half-line (sector) probes
     cat "$OUT/bench$r.json"
   done
   step probe 600 tools/ring_probe 1610612736 w > "$OUT/wr_probe.jsonl" 2> "$OUT/wr_probe.err"
+  [ -n "${PROBE_ONLY:-}" ] && { cat "$OUT/wr_probe.jsonl"; }
   cat "$OUT/wr_probe.jsonl"
   step counters 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
   grep -o -E "TCC_EA0?_RDREQ[A-Z0-9_]*|TCC_BUBBLE[A-Z0-9_]*|TCC_EA0?_WRREQ[A-Z0-9_]*" "$OUT/counters.txt" | sort -u | tr '\n' ' '; echo
   for v in h0 h1; do
-    for pass in "fetch FETCH_SIZE" "rq TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+    for pass in "fetch FETCH_SIZE" "rq TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"; do
       set -- $pass; name=$1; shift
       (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d "$ROOT/$OUT/${v}_$name" \
          -o run --output-format csv -- "$ROOT/tools/ring_probe" 1610612736 $v \
@@ -205,12 +206,28 @@ p)  # HEAD check after the restart; write-cost and half-line (sector) probes
   (cd /tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d "$ROOT/$OUT/clk" \
      -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline \
      > "$ROOT/$OUT/clk.log" 2>&1) || { echo "pmc clk failed"; tail -3 "$OUT/clk.log"; }
-  # the wave's last tile requested up front (OO_RX_PF lines per frame)
-  OO_RX_LIB=build/var_pf16.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q \
-    -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pf_parity.log" 2>&1
-  rc=$?; tail -2 "$OUT/pf_parity.log"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-  ab 3 2 onload_amd/liboo_gpu_rx.so build/var_pf16.so build/var_pf64.so build/var_pfl16.so
-  ab 1 "4 5" onload_amd/liboo_gpu_rx.so build/var_pf16.so
+  ;;
+q)  # write cost by read/store cache policy; half-line reads (HBM request size)
+  step probe 600 tools/ring_probe 1610612736 w > "$OUT/wr_probe.jsonl" 2> "$OUT/wr_probe.err"
+  cat "$OUT/wr_probe.jsonl"
+  [ -n "${SECTOR:-}" ] || { echo "done $(date +%T)"; exit 0; }
+  for v in h0 h1; do
+    for pass in "fetch FETCH_SIZE" "rq TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"; do
+      set -- $pass; name=$1; shift
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d "$ROOT/$OUT/${v}_$name" \
+         -o run --output-format csv -- "$ROOT/tools/ring_probe" 1610612736 $v \
+         > "$ROOT/$OUT/${v}_$name.log" 2>&1) || { echo "pmc $v $name failed"; tail -3 "$OUT/${v}_$name.log"; exit 1; }
+      grep -h '"tag"' "$OUT/${v}_$name.log" || true
+    done
+  done
+  python3 -c "import sys, glob, os; sys.path.insert(0, 'tools'); from pmc_summary import counters; [print(d, counters(d, 'ring_split')) for d in sorted(glob.glob('$OUT/h*_*')) if os.path.isdir(d)]" > "$OUT/sector_summary.txt" 2>&1
+  cat "$OUT/sector_summary.txt"
+  ;;
+r)  # raw per-wave stamps of config 2 (the launch's end); kernel arguments in device memory or not
+  step stamps 300 env OO_RX_LIB=build/var_st.so python tools/stamps.py --config 2 --raw "$OUT/stamps_c2_raw.npz" > "$OUT/stamps_c2.json" 2> "$OUT/stamps.err"
+  cat "$OUT/stamps_c2.json"
+  L=onload_amd/liboo_gpu_rx.so
+  ab 3 2 $L $L@HIP_FORCE_DEV_KERNARG=0
   ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests

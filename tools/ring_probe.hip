@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64) void ring_grp(const u32x4* __restrict__ p, size
 // instructions of eight frames x 128 B, as rx_kernel stages header windows),
 // then the other FB/128 - 1 lines of each frame by 8-lane groups.  HDRLAG:
 // the line-0 reads are for the NEXT tile (as rx_kernel's pipelined staging).
-template <int R, bool HDRLAG, int ST = 0, int HAUX = 0, int SEC = 0>
+template <int R, bool HDRLAG, int ST = 0, int HAUX = 0, int SEC = 0, int BAUX = 2>
 __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, size_t nframes,
                                                  uint32_t* out) {
   constexpr uint32_t fb16 = 96, lines = 12;
@@ -150,6 +150,7 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
   const int g = lane / 8, j = lane % 8;
   const size_t ntiles = nframes / 64;
   uint32_t acc = 0;
+  uint32_t pend = 0;  // ST 11: tiles whose records wait for the next write window
   for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const size_t th = HDRLAG ? t + gridDim.x : t;
     if (th < ntiles) {
@@ -167,19 +168,21 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
       const size_t frame = t * 64 + g + fi * 8;
       return k < total ? p + frame * fb16 + r * 8 + j : p;
     };
+    // SEC: lanes 4-7 of each group read their line's lower half again, so
+    // only the lower 64 B of every body line is requested
+    auto srcs = [&](uint32_t k) {
+      return (SEC != 0 && k < total && j >= 4) ? src(k) - 4 : src(k);
+    };
 #pragma unroll
     for (int u = 0; u < R; ++u)
-      __builtin_amdgcn_global_load_lds((const void*)src(u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void*)srcs(u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, BAUX);
     for (uint32_t k0 = 0; k0 < total; k0 += R) {
 #pragma unroll
       for (int u = 0; u < R; ++u) {
         wait_vm<R - 1>();
         const u32x4 v = lds[u * 64 + lane];
         acc = dot(v.x, dot(v.y, dot(v.z, dot(v.w, acc))));
-        if (SEC == 0 || j < 4)  // SEC: only the lower half of every body line is read
-          __builtin_amdgcn_global_load_lds((const void*)src(k0 + R + u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
-        else
-          __builtin_amdgcn_global_load_lds((const void*)(src(k0 + R + u) - 4), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, 2);
+        __builtin_amdgcn_global_load_lds((const void*)srcs(k0 + R + u), (void __attribute__((address_space(3)))*)(lds + u * 64), 16, 0, BAUX);
       }
     }
     wait_vm<0>();
@@ -207,6 +210,31 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
         u32x4* rq = reinterpret_cast<u32x4*>(out) + 16 + t * 128 + lane;
         rq[0] = r0;
         rq[64] = r0;
+      } else if (ST == 8 || ST == 9 || ST == 10) {  // 8 / 2 tiles' records at once; 4 with nt stores
+        constexpr int K = ST == 8 ? 8 : ST == 9 ? 2 : 4;
+        if ((t / gridDim.x) % K == K - 1) {
+          for (int q = 0; q < K; ++q) {
+            u32x4* rq = reinterpret_cast<u32x4*>(out) + 16 + ((t - q * gridDim.x) * 64 + lane) * 2;
+            if (ST == 10) {
+              __builtin_nontemporal_store(r0, rq);
+              __builtin_nontemporal_store(r0, rq + 1);
+            } else {
+              rq[0] = r0;
+              rq[1] = r0;
+            }
+          }
+        }
+      } else if (ST == 11) {  // all waves write in the same 1.28-us window of every 10.24 us
+        ++pend;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (((now >> 7) & 7u) == 0 || pend >= 8 || t + gridDim.x >= ntiles) {
+          for (uint32_t q = 0; q < pend; ++q) {
+            u32x4* rq = reinterpret_cast<u32x4*>(out) + 16 + ((t - q * gridDim.x) * 64 + lane) * 2;
+            rq[0] = r0;
+            rq[1] = r0;
+          }
+          pend = 0;
+        }
       } else if ((t / gridDim.x) % 4 == 3) {  // 6: four tiles' records at once (8 KB)
         for (int q = 0; q < 4; ++q) {
           u32x4* rq = reinterpret_cast<u32x4*>(out) + 16 + ((t - q * gridDim.x) * 64 + lane) * 2;
@@ -219,7 +247,7 @@ __global__ __launch_bounds__(64) void ring_split(const u32x4* __restrict__ p, si
   if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <int R, bool HDRLAG, int ST = 0, int HAUX = 0, int SEC = 0>
+template <int R, bool HDRLAG, int ST = 0, int HAUX = 0, int SEC = 0, int BAUX = 2>
 static void run_split(const u32x4* a, size_t bytes, uint32_t* o, int cu, const char* tag = "") {
   const size_t lds = (size_t)(R + 8) * 1024;
   const size_t nframes = (bytes - 4096) / 1536 / 64 * 64;
@@ -231,15 +259,15 @@ static void run_split(const u32x4* a, size_t bytes, uint32_t* o, int cu, const c
     float best = 1e9f;
     for (int r = 0; r < 10; ++r) {
       (void)hipEventRecord(e0, 0);
-      hipLaunchKernelGGL((ring_split<R, HDRLAG, ST, HAUX, SEC>), dim3(grid), dim3(64), lds, 0, a, nframes, o);
+      hipLaunchKernelGGL((ring_split<R, HDRLAG, ST, HAUX, SEC, BAUX>), dim3(grid), dim3(64), lds, 0, a, nframes, o);
       (void)hipEventRecord(e1, 0);
       (void)hipEventSynchronize(e1);
       float ms;
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (r >= 2 && ms < best) best = ms;
     }
-    printf("{\"split_hdr\":1,\"tag\":\"%s\",\"hdr_aux\":%d,\"half_lines\":%d,\"hdr_lag\":%d,\"stores\":%d,\"slots\":%d,\"waves_per_cu\":%d,\"ms\":%.4f,\"GBps\":%.1f}\n",
-           tag, HAUX, SEC, (int)HDRLAG, ST, R, m, best, nframes * 1536 / (best * 1e-3) / 1e9);
+    printf("{\"split_hdr\":1,\"tag\":\"%s\",\"hdr_aux\":%d,\"body_aux\":%d,\"half_lines\":%d,\"hdr_lag\":%d,\"stores\":%d,\"slots\":%d,\"waves_per_cu\":%d,\"ms\":%.4f,\"GBps\":%.1f}\n",
+           tag, HAUX, BAUX, SEC, (int)HDRLAG, ST, R, m, best, nframes * 1536 / (best * 1e-3) / 1e9);
   }
 }
 
@@ -280,26 +308,21 @@ int main(int argc, char** argv) {
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
   const int cu = prop.multiProcessorCount;
-  if (argc > 2) {
+  if (argc > 2 && argv[2][0] == 'r') {
     run<8, 1>(a, bytes, o, cu);
     run<16, 1>(a, bytes, o, cu);
     run<32, 1>(a, bytes, o, cu);
   }
-  if (argc > 2 && argv[2][0] == 'w') {  // write-cost and sector experiments (round 3)
-    uint32_t *uc = nullptr, *fg = nullptr;
-    const size_t ob = bytes / 40 + 4096;
-    if (hipExtMallocWithFlags((void**)&uc, ob, hipDeviceMallocUncached) != hipSuccess) uc = nullptr;
-    if (hipExtMallocWithFlags((void**)&fg, ob, hipDeviceMallocFinegrained) != hipSuccess) fg = nullptr;
-    for (int rep = 0; rep < 2; ++rep) {
+  if (argc > 2 && argv[2][0] == 'w') {  // write cost by write grouping (round 3)
+    for (int rep = 0; rep < 3; ++rep) {
       run_split<4, true, 0>(a, bytes, o, cu, "reads");
       run_split<4, true, 1>(a, bytes, o, cu, "records");
-      run_split<4, true, 7>(a, bytes, o, cu, "records_1k_per_instr");
-      run_split<4, true, 0, 2>(a, bytes, o, cu, "reads_all_nt");
-      run_split<4, true, 1, 2>(a, bytes, o, cu, "records_all_nt");
-      run_split<4, true, 7, 2>(a, bytes, o, cu, "records_1k_all_nt");
-      if (uc) run_split<4, true, 1>(a, bytes, uc, cu, "records_uncached_mem");
-      if (fg) run_split<4, true, 1>(a, bytes, fg, cu, "records_finegrained_mem");
-      run_split<4, true, 0, 0, 1>(a, bytes, o, cu, "reads_half_body_lines");
+      run_split<4, true, 9>(a, bytes, o, cu, "records_2tiles");
+      run_split<4, true, 6>(a, bytes, o, cu, "records_4tiles");
+      run_split<4, true, 8>(a, bytes, o, cu, "records_8tiles");
+      run_split<4, true, 10>(a, bytes, o, cu, "records_4tiles_nt");
+      run_split<4, true, 2>(a, bytes, o, cu, "records_nt");
+      run_split<4, true, 11>(a, bytes, o, cu, "records_time_window");
     }
     return 0;
   }

@@ -22,10 +22,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def oo_waves_per_block(lib) -> int:
+    try:
+        return int(lib.oo_rx_waves_per_block())
+    except AttributeError:
+        return 2
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--raw", default="", help="also save the per-wave stamps (npz) here")
     args = ap.parse_args()
     import torch
 
@@ -60,6 +68,10 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     a = st.cpu().numpy().reshape(waves, 128, 16)
     used = a[:, :, 0] != 0
+    if args.raw:
+        kmax = int(used.sum(1).max())
+        np.savez_compressed(args.raw, stamps=a[:, :kmax, :8], grid=grid,
+                            waves_per_block=oo_waves_per_block(lib))
     t0 = a[:, :, 0][used].min()
     ns = 10.0  # s_memrealtime is 100 MHz
     rows = []
@@ -147,10 +159,10 @@ def main() -> None:
                                      for j in range(5)]
                             for k in range(min(int(used.sum(1).max()), 8)) if used[:, k].any()}
     # per-XCD view: blocks are dealt round-robin to the 8 XCDs
-    wpb = max(1, waves // grid)
+    wpb = oo_waves_per_block(lib)
     ends = {}
     for w, k, e, _ in rows:
-        ends.setdefault(int(w) // 4 % 8, []).append(e / 1e3)
+        ends.setdefault(int(w) // wpb % 8, []).append(e / 1e3)
     res["end_us_by_xcd(block%8)"] = {x: round(float(np.mean(v)), 1) for x, v in sorted(ends.items())}
     print(json.dumps(res))
 
