@@ -69,12 +69,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef OO_RX_RING
 #define OO_RX_RING 4  // rx_kernel: body ring slots per wave (even)
 #endif
-#ifndef OO_RX_PF
-#define OO_RX_PF 0  // lines per frame requested up front for a wave's last tile (0: none)
-#endif
-#ifndef OO_RX_PF_LATE
-#define OO_RX_PF_LATE 0  // 1: those requests follow the demux instead of preceding the ring
-#endif
 
 constexpr int WAVES = OO_RX_WAVES;
 constexpr int R = OO_RX_RING;
@@ -258,13 +252,13 @@ __device__ __forceinline__ bool occ_bit(const uint32_t* occ, uint32_t i) {
   return ((occ[i >> 5] >> (i & 31u)) & 1u) != 0;
 }
 
-// ci_sock_intf_check (netif_table.h:30-36) on the socket fields of a slot.
-__device__ __forceinline__ bool bind2dev_ok(const KParams& P, uint32_t sflags, uint64_t hwports,
-                                            int b2d_vlan, int intf_i, int vlan) {
-  if (!(sflags & OO_GPU_RX_SOCK_BIND2DEV)) return true;
-  const uint32_t hw =
-      (intf_i >= 0 && intf_i < OO_GPU_RX_MAX_INTF) ? P.hwport[intf_i] : 0xffu;
-  return hw < 64 && (hwports & (1ull << hw)) != 0 && b2d_vlan == vlan;
+// ci_sock_intf_check (netif_table.h:30-36) on the socket fields of a slot;
+// hwp is the packet's hwport (lane_hwport), 0xff for none.
+__device__ __forceinline__ bool bind2dev_ok(uint32_t sflags, uint64_t hwports, int b2d_vlan,
+                                            uint32_t hwp, int vlan) {
+  // (bitwise, not short-circuit: no branches in the walks' inner step)
+  return !(sflags & OO_GPU_RX_SOCK_BIND2DEV) |
+         ((hwp < 64) & (((hwports >> (hwp & 63u)) & 1u) != 0) & (b2d_vlan == vlan));
 }
 
 // A slot record as loaded: an IPv4 Slot4 in d0..d1, an IPv6 Slot6 in
@@ -328,30 +322,38 @@ __device__ __forceinline__ Probe probe_of(const KParams& P, bool is6) {
 // issuing the next (six memory latencies instead of one).  The wait is
 // vmcnt(0): loads complete in issue order and these are the newest, so it
 // waits for nothing they would not.
-__device__ __forceinline__ void occ_words6(const Probe& t, const uint32_t i[6], uint32_t w[6]) {
+// With them, the lane's byte of the kernel arguments' intf_i_to_hwport
+// table at address ha (netif_table.h:33; a per-lane index, so a vector load,
+// which here costs no wait of its own -- inside the walks its wait would
+// drain the body stream).
+__device__ __forceinline__ void occ_words6(const Probe& t, const uint32_t i[6], uint32_t w[6],
+                                           uint64_t ha, uint32_t& hw) {
   uint64_t a[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) a[k] = t.occ + 4u * (i[k] >> 5);
   asm volatile(
-      "global_load_dword %0, %6, off\n\tglobal_load_dword %1, %7, off\n\t"
-      "global_load_dword %2, %8, off\n\tglobal_load_dword %3, %9, off\n\t"
-      "global_load_dword %4, %10, off\n\tglobal_load_dword %5, %11, off\n\t"
+      "global_load_dword %0, %7, off\n\tglobal_load_dword %1, %8, off\n\t"
+      "global_load_dword %2, %9, off\n\tglobal_load_dword %3, %10, off\n\t"
+      "global_load_dword %4, %11, off\n\tglobal_load_dword %5, %12, off\n\t"
+      "global_load_ubyte %6, %13, off\n\t"
       "s_waitcnt vmcnt(0)"
-      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5])
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5])
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(hw)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(ha)
       : "memory");
 }
 
-__device__ __forceinline__ void occ_words4(const Probe& t, const uint32_t i[4], uint32_t w[4]) {
+__device__ __forceinline__ void occ_words4(const Probe& t, const uint32_t i[4], uint32_t w[4],
+                                           uint64_t ha, uint32_t& hw) {
   uint64_t a[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) a[k] = t.occ + 4u * (i[k] >> 5);
   asm volatile(
-      "global_load_dword %0, %4, off\n\tglobal_load_dword %1, %5, off\n\t"
-      "global_load_dword %2, %6, off\n\tglobal_load_dword %3, %7, off\n\t"
+      "global_load_dword %0, %5, off\n\tglobal_load_dword %1, %6, off\n\t"
+      "global_load_dword %2, %7, off\n\tglobal_load_dword %3, %8, off\n\t"
+      "global_load_ubyte %4, %9, off\n\t"
       "s_waitcnt vmcnt(0)"
-      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(hw)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ha)
       : "memory");
 }
 
@@ -390,16 +392,19 @@ __device__ __forceinline__ Rec load_rec(const KParams& P, const Probe& t, uint32
 template <bool IS6>
 __device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool first4,
                                           const uint32_t la[4], uint32_t lp, const uint32_t ra[4],
-                                          bool ra_null, uint32_t rp, uint32_t proto, int intf_i,
+                                          bool ra_null, uint32_t rp, uint32_t proto, uint32_t hwp,
                                           int vlan, int32_t& id) {
   bool ok;
   uint32_t sflags;
   int b2d;
   uint64_t hw;
+  // (the compares are combined bitwise, not short-circuit: a chain of
+  // branches in the walks' inner step costs more than the compares)
   if (!IS6) {
     const uint32_t st = r.d0.x & ST_MASK;
-    ok = (first4 ? st == ST_PREFERRED : (occupied(st) && (r.d0.w & 0xffffu) == lp)) &&
-         r.d0.y == la[0] && r.d0.z == ra[0] && (r.d0.w >> 16) == rp && (r.d1.x & 0xffu) == proto;
+    const bool stok = first4 ? st == ST_PREFERRED : (occupied(st) & ((r.d0.w & 0xffffu) == lp));
+    ok = stok & (r.d0.y == la[0]) & (r.d0.z == ra[0]) & ((r.d0.w >> 16) == rp) &
+         ((r.d1.x & 0xffu) == proto);
     sflags = r.d1.x >> 16;
     b2d = (int)(int16_t)(r.d1.y & 0xffffu);
     hw = (uint64_t)r.d1.z | ((uint64_t)r.d1.w << 32);
@@ -407,15 +412,16 @@ __device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool f
   } else {
     id = (int32_t)r.d0.x;
     sflags = r.d2.w >> 16;
-    ok = id >= 0 && r.d0.z == la[0] && r.d0.w == la[1] && r.d1.x == la[2] && r.d1.y == la[3] &&
-         (r.d2.z & 0xffffu) == lp && (r.d2.w & 0xffu) == proto &&
-         (ra_null ? !(sflags & OO_GPU_RX_SOCK_CONNECTED)
-                  : (r.d1.z == ra[0] && r.d1.w == ra[1] && r.d2.x == ra[2] && r.d2.y == ra[3] &&
-                     (r.d2.z >> 16) == rp));
+    const bool rok = ra_null ? !(sflags & OO_GPU_RX_SOCK_CONNECTED)
+                             : ((r.d1.z == ra[0]) & (r.d1.w == ra[1]) & (r.d2.x == ra[2]) &
+                                (r.d2.y == ra[3]) & ((r.d2.z >> 16) == rp));
+    ok = (id >= 0) & (r.d0.z == la[0]) & (r.d0.w == la[1]) & (r.d1.x == la[2]) & (r.d1.y == la[3]) &
+         ((r.d2.z & 0xffffu) == lp) & ((r.d2.w & 0xffu) == proto) & rok;
     b2d = (int)(int16_t)(r.d3.x & 0xffffu);
     hw = (uint64_t)r.d3.z | ((uint64_t)r.d3.w << 32);
   }
-  return ok && bind2dev_ok(P, sflags, hw, b2d, intf_i, vlan);
+  (void)P;
+  return ok & bind2dev_ok(sflags, hw, b2d, hwp, vlan);
 }
 
 // One slot against the lookup key for a lane of either family: M = 0 IPv4,
@@ -425,12 +431,12 @@ template <int M>
 __device__ __forceinline__ bool rec_match_m(const KParams& P, const Probe& t, const Rec& r,
                                             bool first4, const uint32_t la[4], uint32_t lp,
                                             const uint32_t ra[4], bool ra_null, uint32_t rp,
-                                            uint32_t proto, int intf_i, int vlan, int32_t& id) {
-  if (M == 0) return rec_match<false>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id);
-  if (M == 1) return rec_match<true>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id);
+                                            uint32_t proto, uint32_t hwp, int vlan, int32_t& id) {
+  if (M == 0) return rec_match<false>(P, r, first4, la, lp, ra, ra_null, rp, proto, hwp, vlan, id);
+  if (M == 1) return rec_match<true>(P, r, first4, la, lp, ra, ra_null, rp, proto, hwp, vlan, id);
   int32_t id4, id6;
-  const bool m4 = rec_match<false>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id4);
-  const bool m6 = rec_match<true>(P, r, first4, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id6);
+  const bool m4 = rec_match<false>(P, r, first4, la, lp, ra, ra_null, rp, proto, hwp, vlan, id4);
+  const bool m6 = rec_match<true>(P, r, first4, la, lp, ra, ra_null, rp, proto, hwp, vlan, id6);
   id = t.is6 ? id6 : id4;
   return t.is6 ? m6 : m4;
 }
@@ -450,7 +456,7 @@ __device__ __forceinline__ bool rec_match_m(const KParams& P, const Probe& t, co
 template <int M>
 __device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_t la[4],
                       uint32_t lp, const uint32_t ra[4], bool ra_null, uint32_t rp, uint32_t proto,
-                      int intf_i, int vlan, uint32_t h1, uint32_t h2, bool occ, Rec rec, bool have,
+                      uint32_t hwp, int vlan, uint32_t h1, uint32_t h2, bool occ, Rec rec, bool have,
                       bool occ_next, bool stop) {
   Match m = {-1, 0};
   const uint32_t first = h1;
@@ -458,7 +464,7 @@ __device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_
   for (uint32_t guard = 0; guard <= t.mask; ++guard) {
     if (!occ) break;  // an EMPTY slot ends the walk
     int32_t id;
-    if (rec_match_m<M>(P, t, rec, guard == 0, la, lp, ra, ra_null, rp, proto, intf_i, vlan, id)) {
+    if (rec_match_m<M>(P, t, rec, guard == 0, la, lp, ra, ra_null, rp, proto, hwp, vlan, id)) {
       if (m.n == 0) m.first = id;
       ++m.n;
       if (stop) break;
@@ -925,7 +931,7 @@ __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, u
 template <int M, bool PRE1>
 __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t, bool any6,
                                                const Hdr& h, uint32_t dport, uint32_t sport,
-                                               uint32_t proto, int intf_i, int vlan, bool tcp,
+                                               uint32_t proto, uint32_t hwp, int vlan, bool tcp,
                                                uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
                                                bool o0, bool o1, bool o2, bool q0, bool q1,
                                                bool q2, Rec rec, int fs, int& stage,
@@ -941,7 +947,7 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
   Rec rec1 = rec;
   const bool pre1 = PRE1 && fs == 0 && o1;
   if (pre1) rec1 = load_rec(P, t, h1_1, any6);
-  Match m = walk<M>(P, t, any6, h.da, dport, h.sa, false, sport, proto, intf_i, vlan, h1_0,
+  Match m = walk<M>(P, t, any6, h.da, dport, h.sa, false, sport, proto, hwp, vlan, h1_0,
                       hash2(dx, dport, sx, sport, proto), o0, rec, fs == 0, q0, tcp);
   DSTAMP(11);
   stage = 1;
@@ -951,7 +957,7 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
   const bool probe = !tcp && !six && m.n == 1;
   s2 = false;
   if (m.n == 0 || probe) {
-    const Match m2 = walk<M>(P, t, any6, h.da, dport, zero, true, 0u, proto, intf_i, vlan, h1_1,
+    const Match m2 = walk<M>(P, t, any6, h.da, dport, zero, true, 0u, proto, hwp, vlan, h1_1,
                              hash2(dx, dport, 0u, 0u, proto), o1, rec1, fs == 1 || pre1, q1,
                              tcp || probe);
     if (probe) {
@@ -963,7 +969,7 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
   }
   DSTAMP(12);
   if (m.n == 0 && tcp) {
-    m = walk<M>(P, t, any6, zero, dport, zero, true, 0u, proto, intf_i, vlan, h1_2,
+    m = walk<M>(P, t, any6, zero, dport, zero, true, 0u, proto, hwp, vlan, h1_2,
                   hash2(0u, dport, 0u, 0u, proto), o2, rec, fs == 2, q2, true);
     stage = 3;
   }
@@ -984,7 +990,7 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
 template <int M>
 __device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bool any6,
                                             const Hdr& h, uint32_t dport, uint32_t sport,
-                                            uint32_t proto, int intf_i, int vlan, bool tcp,
+                                            uint32_t proto, uint32_t hwp, int vlan, bool tcp,
                                             uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
                                             uint32_t h2_0, uint32_t h2_1, uint32_t h2_2, bool o0,
                                             bool o1, bool o2, bool q0, bool q1, bool q2, Rec rec,
@@ -1020,7 +1026,7 @@ __device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bo
         }
         int32_t id;
         if (rec_match_m<M>(P, t, rec, k == 0, la, dport, ra, !st0, st0 ? sport : 0u, proto,
-                           intf_i, vlan, id)) {
+                           hwp, vlan, id)) {
           if (probe) {
             s2 = true;
             end = true;
@@ -1106,6 +1112,13 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
   if (__ballot(look) != 0) {
     constexpr bool any6 = ANY6;
     const Probe t = probe_of(P, ANY6 && is6);
+    // (intf_i_to_hwport for a valid interface; lanes with none read entry 0
+    // and take 0xff)
+    const bool intf_ok = (uint32_t)intf_i < (uint32_t)OO_GPU_RX_MAX_INTF;
+    // (the kernel's one argument, KParams, starts the argument segment)
+    const uint64_t hwa = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) +
+                         offsetof(KParams, hwport) + (intf_ok ? (uint32_t)intf_i : 0u);
+    uint32_t hwp = 0xffu;
     const bool tcp = proto == 6u;
     const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & t.mask;
     const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & t.mask;
@@ -1120,13 +1133,13 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     if (look) {
       const uint32_t idx[6] = {h1_0, h1_1, h1_2, (h1_0 + h2_0) & t.mask, (h1_1 + h2_1) & t.mask,
                                (h1_2 + h2_2) & t.mask};
-      uint32_t w[6];
+      uint32_t w[6], hw;
       if (any_tcp) {
-        occ_words6(t, idx, w);
+        occ_words6(t, idx, w, hwa, hw);
       } else {
         const uint32_t i4[4] = {idx[0], idx[1], idx[3], idx[4]};
         uint32_t w4[4];
-        occ_words4(t, i4, w4);
+        occ_words4(t, i4, w4, hwa, hw);
         w[0] = w4[0];
         w[1] = w4[1];
         w[3] = w4[2];
@@ -1134,6 +1147,7 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
         w[2] = w[5] = 0u;
       }
       DSTAMP(8);
+      hwp = intf_ok ? (hw & 0xffu) : 0xffu;
       auto bit = [&](int k) { return ((w[k] >> (idx[k] & 31u)) & 1u) != 0; };
       o0 = bit(0);
       o1 = bit(1);
@@ -1155,11 +1169,11 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
       // Waves with TCP lookups (three stages, long connected-socket chains)
       // take the state machine; UDP-only waves the stage-by-stage walks.
       if (OO_RX_FSM && any_tcp)
-        m = lookup_fsm<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp, h1_0, h1_1,
+        m = lookup_fsm<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, hwp, vlan, tcp, h1_0, h1_1,
                                      h1_2, h2_0, h2_1, h2_2, o0, o1, o2, q0, q1, q2, rec, fs, stage,
                                      s2);
       else
-        m = lookup_stages<ANY6 ? 2 : 0, !ANY6>(P, t, any6, h, dport, sport, proto, intf_i, vlan, tcp,
+        m = lookup_stages<ANY6 ? 2 : 0, !ANY6>(P, t, any6, h, dport, sport, proto, hwp, vlan, tcp,
                                                h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs, stage,
                                                s2);
       DSTAMP(10);
@@ -1871,9 +1885,6 @@ struct WaveLds {
   uint32_t cnt[OO_RX_R_COUNT];  // per-reason counts
   uint32_t dbase, gofs;          // claims: first dynamic tile of the group, counter offset
   uint32_t T0, pad;              // the tile's body rounds (kept out of the registers)
-#if OO_RX_PF
-  uint32_t pf[64];               // landing place of the last tile's line requests (unread)
-#endif
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
 constexpr int WAVE_U4 = (int)(sizeof(WaveLds) / 16);
@@ -2032,35 +2043,12 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     if (lane == 0) lds_write4(&L.T0, T0);
     IssueCursor ci;
     if (T0 != 0) issue_slot(ci, J, 0, lane, zero);  // (body-less tiles issue no rounds)
-#if OO_RX_PF && !OO_RX_PF_LATE
-    // The wave's last tile: every line of its frames' bodies (at most
-    // OO_RX_PF per frame) is requested up front by 4-B LDS-DMA requests of the
-    // default policy, which leave the lines in L2 and the Infinity Cache; the
-    // ring below then reads them from there.  The launch ends with waves
-    // streaming their last tiles while others have finished: their ring
-    // depth, not HBM, bounds that stretch.
-    uint32_t npf = 0;
-    if (!TX && T0 != 0 && tnext >= P.ntiles) {
-      const uint32_t off0 = body_off0(dv.abase);
-      const uint32_t nl = dv.span > HB ? ((uint32_t)dv.span - off0 + 127u) >> 7 : 0u;
-      npf = min(wave_max(nl, lane), (uint32_t)OO_RX_PF);
-      const uint64_t a0 = dv.abase + off0;
-      for (uint32_t k = 0; k < npf; ++k) {
-        const uint64_t a = nl != 0 ? a0 + 128u * min(k, nl - 1u) : zero;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(a), (lptr)(&L.pf[0]), 4, 0, 0);
-      }
-    }
-#else
-    constexpr uint32_t npf = 0;
-#endif
     // This tile's header windows: older than the previous tile's NST stores
-    // (none before the first tile), the last tile's line requests and the R
-    // rounds issued here.
+    // (none before the first tile) and the R rounds issued here.
     if (T != 0) {
 #pragma unroll
       for (int u = 0; u < R; ++u) issue_round(ci, J, zero, &L.ring[u][0], lane);
-      if (npf != 0) vm_wait_n((it_ == 0 ? R : R + NSTK) + (int)npf);
-      else if (it_ == 0) vm_wait<R>();
+      if (it_ == 0) vm_wait<R>();
       else vm_wait<R + NSTK>();
     } else {
       if (it_ == 0) vm_wait<0>();
@@ -2110,22 +2098,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     T0 = sreg(lds_read4(&L.T0));
     ext = E > 0 && T0 > (uint32_t)(R + E);
     T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
-#if OO_RX_PF && OO_RX_PF_LATE
-    // (late form: the demux's loads are not queued behind these requests)
-    uint32_t npl = 0;
-    if (!TX && T0 != 0 && tnext >= P.ntiles) {
-      const uint32_t off0 = body_off0(dv.abase);
-      const uint32_t nl = dv.span > HB ? ((uint32_t)dv.span - off0 + 127u) >> 7 : 0u;
-      npl = min(wave_max(nl, lane), (uint32_t)min(OO_RX_PF, 16));
-      const uint64_t a0 = dv.abase + off0;
-      for (uint32_t k = 0; k < npl; ++k) {
-        const uint64_t a = nl != 0 ? a0 + 128u * min(k, nl - 1u) : zero;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(a), (lptr)(&L.pf[0]), 4, 0, 0);
-      }
-    }
-#else
-    constexpr uint32_t npl = 0;
-#endif
     // Tile i + 2: the claim issued at the previous tile, read at its end
     // (have) or, after a tile without a body, here (the compiler waits for
     // it: vmcnt(0), which a body-less tile has little in flight to pay for).
@@ -2173,8 +2145,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       // line and the claim, and the refills so far -- R + E in all.
 #pragma unroll
       for (int u = 0; u < R; u += 2) {
-        if (npl != 0) vm_wait_n(R + E + (int)npl);
-        else vm_wait<R + E>();
+        vm_wait<R + E>();
         uint4 v0, v1;
         lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
         consume_round(cc, J, v0, lane);
@@ -2186,7 +2157,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       // line and the claim, and the R refills.
 #pragma unroll
       for (int u = 0; u < E; u += 2) {
-        vm_wait_n(R + E - u + (int)npl);
+        vm_wait_n(R + E - u);
         uint4 v0, v1;
         lds_read16x2(&L.hdr[u][lane], &L.hdr[u + 1][lane], v0, v1);
         consume_round(cc, J, v0, lane);
@@ -2197,7 +2168,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // The ring loop (T is a multiple of R).  Newer than the awaited pair: the
     // rest of the ring, plus in the first turn the staging operations issued
     // since the ring was filled (NHS, or HC after an ext prefix); none past T.
-    const int nhs = ext ? HC : NHS + (int)npl;
+    const int nhs = ext ? HC : NHS;
     for (uint32_t k0 = 0; k0 < T; k0 += R) {
       const bool first = k0 == 0, last = k0 + R == T;
 #pragma unroll

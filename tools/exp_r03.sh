@@ -229,6 +229,11 @@ r)  # raw per-wave stamps of config 2 (the launch's end); kernel arguments in de
   L=onload_amd/liboo_gpu_rx.so
   ab 3 2 $L $L@HIP_FORCE_DEV_KERNARG=0
   ;;
+s)  # per-tile hwport byte + branch-free slot compares vs HEAD: full GPU suite, then A/B
+  tests
+  ab 2 "2 3 5" onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ab 1 4 onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
   for r in 1 2; do
