@@ -75,6 +75,9 @@ def parse_args(argv=None):
     ap.add_argument("--n", type=int, default=0, help="packets per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--steady", type=int, default=200,
+                    help="side measurement after the timed region: this many more launches, "
+                         "event-timed (0: skip); reported as 'steady', never as value")
     ap.add_argument("--scatter", action="store_true",
                     help="N>1: also time an RCCL scatter of every shard from rank 0's GPU")
     ap.add_argument("--tx", action="store_true",
@@ -258,6 +261,27 @@ def run_rank(args) -> None:
     else:
         ms_step, kern_ms_max = local_ms, kern_ms
 
+    # Side measurement, after the timed region: the same launch repeated
+    # --steady times.  The GPU's clock settles several milliseconds after it
+    # becomes busy (2.0-2.1 GHz around launches 7-19,
+    # 2.35-2.47 GHz from about the 30th), so K = 20 launches after W = 5 sit
+    # in that dip; this shows the settled per-launch time next to it.  It is
+    # never `value` or `roofline`.
+    steady = None
+    if args.steady > 0:
+        es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        es0.record(stream)
+        for _ in range(args.steady):
+            step()
+        es1.record(stream)
+        torch.cuda.synchronize(dev)
+        st_ms = float(es0.elapsed_time(es1)) / args.steady
+        st_mean = float(desc["len"].astype(np.float64).mean()) if n else 0.0
+        steady = {"launches": args.steady, "after_launches": args.warmup + args.steps,
+                  "kernel_ms": round(st_ms, 5),
+                  "frac": round((st_mean + DESC_B + RESULT_B) * n / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
     # What was timed is checked: one more pass with counters; N>1 gathers
     # every rank's records to rank 0 (outside the timed region).
     stack.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
@@ -299,6 +323,8 @@ def run_rank(args) -> None:
             traffic = None
 
     extras = {}
+    if steady is not None:
+        extras["steady"] = steady
     if table_bcast is not None:
         extras["table_broadcast"] = table_bcast
     if gather is not None:

@@ -756,11 +756,14 @@ __device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int
   const int ip_paylen = (int)ip_len - 20;
   const uint32_t udp_len = bswap16(c[2].y >> 16);
   const int hlen = (int)(((c[2].w >> 16) & 0xf0u) >> 2);
-  bool ok = shift == 0 && off0 >= 48 && len >= 48 && (c[0].w & 0x000fffffu) == 0x00050008u &&
-            ip_paylen > 0 && len >= 14 + (int)ip_len && (frag & 0x3fffu) == 0u;
+  // (gates combined bitwise: one branch, not one per test)
   const bool tcp = proto == 6u;
-  ok = ok && (tcp ? (ip_paylen >= 20 && hlen >= 20 && ip_paylen >= hlen)
-                  : (proto == 17u && ip_paylen >= 8 && udp_len >= 8u && udp_len <= (uint32_t)ip_paylen));
+  const bool ok = (shift == 0) & (off0 >= 48) & (len >= 48) &
+                  ((c[0].w & 0x000fffffu) == 0x00050008u) & (ip_paylen > 0) &
+                  (len >= 14 + (int)ip_len) & ((frag & 0x3fffu) == 0u) &
+                  (tcp ? ((ip_paylen >= 20) & (hlen >= 20) & (ip_paylen >= hlen))
+                       : ((proto == 17u) & (ip_paylen >= 8) & (udp_len >= 8u) &
+                          (udp_len <= (uint32_t)ip_paylen)));
   if (!ok) return false;
   const uint32_t ucs = c[2].z & 0xffffu;  // UDP checksum field (0: none, IPv4)
   const bool need_l4 = tcp || ucs != 0u;
@@ -825,10 +828,11 @@ __device__ __forceinline__ bool parse_fixed6(const uint4 (&c)[HC], int shift, in
   const uint32_t udp_len = bswap16(c[3].z >> 16);
   const int hlen = (int)(((c[4].x >> 16) & 0xf0u) >> 2);
   const bool tcp = proto == 6u;
-  bool ok = shift == 0 && off0 >= 64 && (c[0].w & 0xffffu) == 0xdd86u && ip_paylen > 0 &&
-            len >= 54 + ip_paylen;
-  ok = ok && (tcp ? (ip_paylen >= 20 && hlen >= 20 && ip_paylen >= hlen)
-                  : (proto == 17u && ip_paylen >= 8 && udp_len >= 8u && udp_len <= (uint32_t)ip_paylen));
+  const bool ok = (shift == 0) & (off0 >= 64) & ((c[0].w & 0xffffu) == 0xdd86u) & (ip_paylen > 0) &
+                  (len >= 54 + ip_paylen) &
+                  (tcp ? ((ip_paylen >= 20) & (hlen >= 20) & (ip_paylen >= hlen))
+                       : ((proto == 17u) & (ip_paylen >= 8) & (udp_len >= 8u) &
+                          (udp_len <= (uint32_t)ip_paylen)));
   if (!ok) return false;
   const int E4 = 54 + (tcp ? ip_paylen : (int)udp_len);
   // Pseudo header (checksum.c:215-223): the 16 address words [22, 54), then

@@ -234,6 +234,9 @@ s)  # per-tile hwport byte + branch-free slot compares vs HEAD: full GPU suite, 
   ab 2 "2 3 5" onload_amd/liboo_gpu_rx.so build/var_ref.so
   ab 1 4 onload_amd/liboo_gpu_rx.so build/var_ref.so
   ;;
+t)  # 8 waves per CU (the check builds: ring 6 / 8, LDS allows 4 blocks per CU) vs the product
+  ab 3 2 onload_amd/liboo_gpu_rx.so build/check/liboo_gpu_rx_r8e2.so build/check/liboo_gpu_rx_r6e4.so
+  ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
   for r in 1 2; do
