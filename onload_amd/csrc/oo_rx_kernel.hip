@@ -69,6 +69,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef OO_RX_RING
 #define OO_RX_RING 4  // rx_kernel: body ring slots per wave (even)
 #endif
+#ifndef OO_RX_GSEQ
+#define OO_RX_GSEQ 0  // 1: per-group job sequences instead of lockstep job slots
+#endif
 
 constexpr int WAVES = OO_RX_WAVES;
 constexpr int R = OO_RX_RING;
@@ -1337,7 +1340,8 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
   }
   uint32_t myq;
   const uint32_t r0 = bm ? (uint32_t)__builtin_amdgcn_readlane((int)rounds, __builtin_ctzll(bm)) : 0u;
-  if (__ballot(nb != 0 && rounds != r0) == 0) {  // all jobs alike: list order
+  const bool alike = __ballot(nb != 0 && rounds != r0) == 0;
+  if (alike) {  // all jobs alike: list order
     const uint32_t M = (uint32_t)__popcll(bm);
     const uint32_t below = __builtin_amdgcn_mbcnt_hi(
         (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
@@ -1345,7 +1349,45 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
   } else {
     myq = rank_desc(rounds, lane, 32 - __builtin_clz(wave_max(rounds, lane)));
   }
+#if OO_RX_GSEQ
+  // Job q (by size, largest first) goes to group g at position p = q / 8:
+  // every group holds eight jobs, one from each pass of eight.
+  {
+    const uint32_t p = myq >> 3, i = myq & 7u;
+    // snake order (0..7, 7..0, ...): the groups' round totals come out alike
+    myslot = ((p & 1u) ? 7u - i : i) * 8u + p;
+  }
+#if OO_RX_GSEQ == 2
+  if (!alike) {
+    // Longest job first, by passes: pass p's eight jobs go to the groups in
+    // the order of their loads so far, the largest job to the least loaded
+    // group (config 4: 114 rounds per tile against the snake's 122, 111 at
+    // best).  Lanes 0..7 hold the groups' loads; lane q, in rank order, the
+    // rounds of job q.
+    const uint32_t rk = (uint32_t)__builtin_amdgcn_ds_permute((int)(myq << 2), (int)rounds);
+    uint32_t G = 0, grp = 0;
+#pragma unroll 1
+    for (uint32_t p = 0; p < 8u; ++p) {
+      uint32_t r = 0;  // lanes 0..7: the group's place by load (ties by index)
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const uint32_t gh = (uint32_t)__builtin_amdgcn_readlane((int)G, h);
+        r += (gh < G || (gh == G && (uint32_t)h < lane)) ? 1u : 0u;
+      }
+      const uint32_t take = lane_get(rk, 8u * p + (r & 7u));
+      if (lane < 8u) G += take;
+      // lane i < 8: the group in place i; the pass's job lanes learn theirs
+      const uint32_t inv = (uint32_t)__builtin_amdgcn_ds_permute(
+          (int)((lane < 8u ? r : lane) << 2), (int)lane);
+      const uint32_t g = lane_get(inv, lane & 7u);
+      if ((lane >> 3) == p) grp = g;
+    }
+    myslot = lane_get(grp, myq) * 8u + (myq >> 3);
+  }
+#endif
+#else
   myslot = (myq & 7u) * 8u + (myq >> 3);
+#endif
   const uint32_t jp = (uint32_t)__builtin_amdgcn_ds_permute((int)(myslot << 2), (int)lane);
   const uint64_t a0 = abase + off0;
   Jobs J;
@@ -1353,12 +1395,137 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
   J.hi = lane_get((uint32_t)(a0 >> 32), jp);
   J.nb = lane_get(nb, jp);
   J.lim = lane_get((uint32_t)span - off0, jp);
+#if OO_RX_GSEQ
+  // this lane's job's rounds; the tile takes the longest group's total
+  J.rj = (J.nb + 7u) >> 3;
+  J.T = wave_max(group_sum8(J.rj), lane);
+#else
   // R_j: the most rounds over lanes 8g + j
   J.rj = max_x8((J.nb + 7u) >> 3);
   J.T = (uint32_t)__builtin_amdgcn_readlane((int)group_sum8(J.rj), 0);
+#endif
   return J;
 }
 
+#if OO_RX_GSEQ
+// Per-group job sequences (OO_RX_GSEQ): each 8-lane group streams its eight
+// jobs back to back and moves to its next job on its own round, so a round
+// carries every group's line until the group's sequence ends (lockstep job
+// slots wait for the slot's longest job: config 4 carries 142 rounds of
+// lines per tile for 111 rounds of bytes).  The cursors are per lane (one
+// value per group); a group past its last job reads the zero line.
+constexpr uint32_t NOJOB = 0xffffffffu;  // rounds of "no job": never reached
+
+struct IssueCursor {
+  uint32_t js, rnd, R;  // the group's job position, round in the job, its rounds
+  uint32_t adv;         // rounds after which a stops advancing
+  uint64_t a;           // the chunk this lane reads next
+};
+
+// Point the cursor at position js of the lane's group.  A lane past its
+// job's last chunk keeps reading that chunk (a line of the same job); a
+// group with no job there reads the zero line.  All lanes active.
+__device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32_t js,
+                                           uint32_t lane, uint64_t zero) {
+  const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
+  const uint32_t nb0 = lane_get(J.nb, s), lo = lane_get(J.lo, s), hi = lane_get(J.hi, s);
+  const uint32_t nb = js < 8u ? nb0 : 0u;
+  c.js = js;
+  c.rnd = 0;
+  c.R = nb != 0 ? (nb + 7u) >> 3 : NOJOB;
+  const bool own = nb > gj;
+  c.adv = own ? (nb - gj - 1u) >> 3 : 0u;
+  const uint64_t a0 = (uint64_t)hi << 32 | lo;
+  c.a = nb == 0 ? zero : a0 + (own ? gj : nb - 1u) * 16u;
+}
+
+// Issues the cursor's round into `slot`; groups whose job ends move on.
+__device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint64_t zero,
+                                            void* slot, uint32_t lane) {
+  glds<OO_RX_BODY_AUX>(c.a, slot);
+  c.a += c.rnd < c.adv ? 128u : 0u;
+  const bool sw = ++c.rnd == c.R;
+  if (__ballot(sw) != 0) {
+    IssueCursor n;
+    issue_slot(n, J, c.js + 1u, lane, zero);
+    if (sw) c = n;
+  }
+}
+
+struct ConsumeCursor {
+  uint32_t js, rnd, R;  // per group, as IssueCursor
+  uint32_t lv;          // rounds of the job in which this lane has a chunk
+  uint32_t vb;          // bytes of its last chunk in the frame (1..16)
+  uint4 m;              // byte mask of its last chunk
+  uint32_t acc;         // this lane's running sum
+  uint32_t bs;          // the total of job (group, lane & 7); 0 if none
+};
+
+__device__ __forceinline__ void consume_slot(ConsumeCursor& c, const Jobs& J, uint32_t js,
+                                             uint32_t lane) {
+  const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
+  const uint32_t nb0 = lane_get(J.nb, s), lim = lane_get(J.lim, s);
+  const uint32_t nb = js < 8u ? nb0 : 0u;
+  c.js = js;
+  c.rnd = 0;
+  c.R = nb != 0 ? (nb + 7u) >> 3 : NOJOB;
+  c.lv = nb > gj ? (nb - gj + 7u) >> 3 : 0u;
+  const int last = 16 * (int)(gj + 8u * (c.lv - 1u));  // this lane's last chunk
+  c.vb = (uint32_t)min(max((int)lim - last, 0), 16);
+  auto bytes = [](int k) -> uint32_t {
+    return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * k)) - 1u;
+  };
+  const int vb = (int)c.vb;
+  c.m = make_uint4(bytes(vb), bytes(vb - 4), bytes(vb - 8), bytes(vb - 12));
+}
+
+__device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, uint32_t lane) {
+  consume_slot(c, J, 0, lane);
+  c.acc = 0;
+  c.bs = 0;
+}
+
+// Consumes one round from the landed bytes v (lanes past their chunks weigh
+// their words by 0); a group whose job ends folds its eight lane sums into
+// the job's lane and moves on.
+__device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
+                                              uint32_t lane) {
+  const bool live = c.rnd < c.lv;
+  const bool part = live && c.rnd + 1u == c.lv && c.vb != 16u;
+  if (__ballot(part) == 0) {
+    const uint32_t w = live ? 0x00010001u : 0u;
+    uint32_t a = dot(v.x, w, c.acc);
+    uint32_t b = dot(v.y, w, 0u);
+    a = dot(v.z, w, a);
+    b = dot(v.w, w, b);
+    c.acc = a + b;
+  } else {  // some lane holds a frame's partial last chunk: byte masks
+    const uint32_t f = live ? 0xffffffffu : 0u;
+    const uint4 mm = part ? c.m : make_uint4(f, f, f, f);
+    uint32_t a = dot(v.x & mm.x, 0x00010001u, c.acc);
+    uint32_t b = dot(v.y & mm.y, 0x00010001u, 0u);
+    a = dot(v.z & mm.z, 0x00010001u, a);
+    b = dot(v.w & mm.w, 0x00010001u, b);
+    c.acc = a + b;
+  }
+  const bool end = ++c.rnd == c.R;
+  if (__ballot(end) != 0) {
+    const uint32_t t = group_sum8(c.acc);
+    ConsumeCursor n;
+    consume_slot(n, J, c.js + 1u, lane);
+    if (end) {
+      if ((lane & 7u) == c.js) c.bs = t;
+      c.acc = 0;
+      c.js = n.js;
+      c.rnd = 0;
+      c.R = n.R;
+      c.lv = n.lv;
+      c.vb = n.vb;
+      c.m = n.m;
+    }
+  }
+}
+#else
 __device__ __forceinline__ uint32_t slot_rounds(const Jobs& J, uint32_t js) {
   return js < 8u ? (uint32_t)__builtin_amdgcn_readlane((int)J.rj, (int)js) : 0u;
 }
@@ -1473,6 +1640,8 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
     consume_slot(c, J, c.js + 1, lane);
   }
 }
+
+#endif  // OO_RX_GSEQ
 
 // Tiles.  The batch is cut into P.ntiles tiles, K per tile-processing wave
 // (rx_kernel's waves), which take tiles w, w + W, ...
