@@ -1307,6 +1307,16 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v, uint32_t lane) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0xb1, 0xf, 0xf, false));   // [1,0,3,2]
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0x4e, 0xf, 0xf, false));   // [2,3,0,1]
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0x141, 0xf, 0xf, false));  // half mirror
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
+  v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401f));  // lane ^ 16
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // lane ^ 32
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)min((uint32_t)p[0], (uint32_t)p[1]));
+}
+
 // Rank of each lane's key among the wave's, largest first, ties in lane
 // order (a stable LSD radix sort on ballots; `bits` wave-uniform).
 __device__ __forceinline__ uint32_t rank_desc(uint32_t key, uint32_t lane, int bits) {
@@ -1357,34 +1367,6 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
     // snake order (0..7, 7..0, ...): the groups' round totals come out alike
     myslot = ((p & 1u) ? 7u - i : i) * 8u + p;
   }
-#if OO_RX_GSEQ == 2
-  if (!alike) {
-    // Longest job first, by passes: pass p's eight jobs go to the groups in
-    // the order of their loads so far, the largest job to the least loaded
-    // group (config 4: 114 rounds per tile against the snake's 122, 111 at
-    // best).  Lanes 0..7 hold the groups' loads; lane q, in rank order, the
-    // rounds of job q.
-    const uint32_t rk = (uint32_t)__builtin_amdgcn_ds_permute((int)(myq << 2), (int)rounds);
-    uint32_t G = 0, grp = 0;
-#pragma unroll 1
-    for (uint32_t p = 0; p < 8u; ++p) {
-      uint32_t r = 0;  // lanes 0..7: the group's place by load (ties by index)
-#pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const uint32_t gh = (uint32_t)__builtin_amdgcn_readlane((int)G, h);
-        r += (gh < G || (gh == G && (uint32_t)h < lane)) ? 1u : 0u;
-      }
-      const uint32_t take = lane_get(rk, 8u * p + (r & 7u));
-      if (lane < 8u) G += take;
-      // lane i < 8: the group in place i; the pass's job lanes learn theirs
-      const uint32_t inv = (uint32_t)__builtin_amdgcn_ds_permute(
-          (int)((lane < 8u ? r : lane) << 2), (int)lane);
-      const uint32_t g = lane_get(inv, lane & 7u);
-      if ((lane >> 3) == p) grp = g;
-    }
-    myslot = lane_get(grp, myq) * 8u + (myq >> 3);
-  }
-#endif
 #else
   myslot = (myq & 7u) * 8u + (myq >> 3);
 #endif
@@ -1414,63 +1396,85 @@ __device__ __forceinline__ Jobs jobs_setup(uint64_t abase, int span, uint32_t la
 // slots wait for the slot's longest job: config 4 carries 142 rounds of
 // lines per tile for 111 rounds of bytes).  The cursors are per lane (one
 // value per group); a group past its last job reads the zero line.
-constexpr uint32_t NOJOB = 0xffffffffu;  // rounds of "no job": never reached
+constexpr uint32_t NOJOB = 0xffffffffu;  // "no job": a round never reached
 
+// Rounds are counted per cursor in k, wave-uniform (one scalar add a round);
+// each lane keeps the rounds at which its group's job ends and after which
+// its own chunk stops advancing as absolute counts, so a round costs one
+// vector compare more than the lockstep slots.
 struct IssueCursor {
-  uint32_t js, rnd, R;  // the group's job position, round in the job, its rounds
-  uint32_t adv;         // rounds after which a stops advancing
-  uint64_t a;           // the chunk this lane reads next
+  uint32_t k;       // rounds issued (wave-uniform)
+  uint32_t knext;   // the first kend over the groups (wave-uniform)
+  uint32_t js;      // the group's job position
+  uint32_t kend;    // k at which the group's job ends (NOJOB: none)
+  uint32_t kadv;    // k after which a stops advancing
+  uint64_t a;       // the chunk this lane reads next
 };
 
-// Point the cursor at position js of the lane's group.  A lane past its
-// job's last chunk keeps reading that chunk (a line of the same job); a
-// group with no job there reads the zero line.  All lanes active.
-__device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32_t js,
-                                           uint32_t lane, uint64_t zero) {
+// Point the cursor at position js of the lane's group, at round k.  A lane
+// past its job's last chunk keeps reading that chunk (a line of the same
+// job); a group with no job there reads the zero line.  All lanes active.
+__device__ __forceinline__ void issue_job(IssueCursor& c, const Jobs& J, uint32_t js,
+                                          uint32_t lane, uint64_t zero) {
   const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
   const uint32_t nb0 = lane_get(J.nb, s), lo = lane_get(J.lo, s), hi = lane_get(J.hi, s);
   const uint32_t nb = js < 8u ? nb0 : 0u;
-  c.js = js;
-  c.rnd = 0;
-  c.R = nb != 0 ? (nb + 7u) >> 3 : NOJOB;
   const bool own = nb > gj;
-  c.adv = own ? (nb - gj - 1u) >> 3 : 0u;
+  c.js = js;
+  c.kend = nb != 0 ? c.k + ((nb + 7u) >> 3) : NOJOB;
+  c.kadv = c.k + (own ? (nb - gj - 1u) >> 3 : 0u);
   const uint64_t a0 = (uint64_t)hi << 32 | lo;
   c.a = nb == 0 ? zero : a0 + (own ? gj : nb - 1u) * 16u;
+}
+
+__device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32_t js,
+                                           uint32_t lane, uint64_t zero) {
+  c.k = 0;
+  issue_job(c, J, js, lane, zero);
+  c.knext = wave_min(c.kend);
 }
 
 // Issues the cursor's round into `slot`; groups whose job ends move on.
 __device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint64_t zero,
                                             void* slot, uint32_t lane) {
   glds<OO_RX_BODY_AUX>(c.a, slot);
-  c.a += c.rnd < c.adv ? 128u : 0u;
-  const bool sw = ++c.rnd == c.R;
-  if (__ballot(sw) != 0) {
+  c.a += c.k < c.kadv ? 128u : 0u;
+  if (++c.k == c.knext) {  // some group's job ends (a scalar test per round)
+    const bool sw = c.k == c.kend;
     IssueCursor n;
-    issue_slot(n, J, c.js + 1u, lane, zero);
-    if (sw) c = n;
+    n.k = c.k;
+    issue_job(n, J, c.js + 1u, lane, zero);
+    if (sw) {
+      c.js = n.js;
+      c.kend = n.kend;
+      c.kadv = n.kadv;
+      c.a = n.a;
+    }
+    c.knext = wave_min(c.kend);
   }
 }
 
 struct ConsumeCursor {
-  uint32_t js, rnd, R;  // per group, as IssueCursor
-  uint32_t lv;          // rounds of the job in which this lane has a chunk
+  uint32_t k;           // rounds consumed (wave-uniform)
+  uint32_t knext;       // the first kend over the groups (wave-uniform)
+  uint32_t js, kend;    // per group, as IssueCursor
+  uint32_t klv;         // k up to which this lane has chunks of the job
   uint32_t vb;          // bytes of its last chunk in the frame (1..16)
   uint4 m;              // byte mask of its last chunk
   uint32_t acc;         // this lane's running sum
   uint32_t bs;          // the total of job (group, lane & 7); 0 if none
 };
 
-__device__ __forceinline__ void consume_slot(ConsumeCursor& c, const Jobs& J, uint32_t js,
-                                             uint32_t lane) {
+__device__ __forceinline__ void consume_job(ConsumeCursor& c, const Jobs& J, uint32_t js,
+                                            uint32_t lane) {
   const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
   const uint32_t nb0 = lane_get(J.nb, s), lim = lane_get(J.lim, s);
   const uint32_t nb = js < 8u ? nb0 : 0u;
+  const uint32_t lv = nb > gj ? (nb - gj + 7u) >> 3 : 0u;  // rounds with a chunk
   c.js = js;
-  c.rnd = 0;
-  c.R = nb != 0 ? (nb + 7u) >> 3 : NOJOB;
-  c.lv = nb > gj ? (nb - gj + 7u) >> 3 : 0u;
-  const int last = 16 * (int)(gj + 8u * (c.lv - 1u));  // this lane's last chunk
+  c.kend = nb != 0 ? c.k + ((nb + 7u) >> 3) : NOJOB;
+  c.klv = c.k + lv;
+  const int last = 16 * (int)(gj + 8u * (lv - 1u));  // this lane's last chunk
   c.vb = (uint32_t)min(max((int)lim - last, 0), 16);
   auto bytes = [](int k) -> uint32_t {
     return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * k)) - 1u;
@@ -1480,7 +1484,9 @@ __device__ __forceinline__ void consume_slot(ConsumeCursor& c, const Jobs& J, ui
 }
 
 __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, uint32_t lane) {
-  consume_slot(c, J, 0, lane);
+  c.k = 0;
+  consume_job(c, J, 0, lane);
+  c.knext = wave_min(c.kend);
   c.acc = 0;
   c.bs = 0;
 }
@@ -1490,8 +1496,8 @@ __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, u
 // the job's lane and moves on.
 __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
                                               uint32_t lane) {
-  const bool live = c.rnd < c.lv;
-  const bool part = live && c.rnd + 1u == c.lv && c.vb != 16u;
+  const bool live = c.k < c.klv;
+  const bool part = live && c.k + 1u == c.klv && c.vb != 16u;
   if (__ballot(part) == 0) {
     const uint32_t w = live ? 0x00010001u : 0u;
     uint32_t a = dot(v.x, w, c.acc);
@@ -1508,21 +1514,22 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
     b = dot(v.w & mm.w, 0x00010001u, b);
     c.acc = a + b;
   }
-  const bool end = ++c.rnd == c.R;
-  if (__ballot(end) != 0) {
+  if (++c.k == c.knext) {  // some group's job ends (a scalar test per round)
+    const bool end = c.k == c.kend;
     const uint32_t t = group_sum8(c.acc);
     ConsumeCursor n;
-    consume_slot(n, J, c.js + 1u, lane);
+    n.k = c.k;
+    consume_job(n, J, c.js + 1u, lane);
     if (end) {
       if ((lane & 7u) == c.js) c.bs = t;
       c.acc = 0;
       c.js = n.js;
-      c.rnd = 0;
-      c.R = n.R;
-      c.lv = n.lv;
+      c.kend = n.kend;
+      c.klv = n.klv;
       c.vb = n.vb;
       c.m = n.m;
     }
+    c.knext = wave_min(c.kend);
   }
 }
 #else

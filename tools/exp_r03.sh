@@ -238,13 +238,14 @@ t)  # 8 waves per CU (the check builds: ring 6 / 8, LDS allows 4 blocks per CU) 
   ab 3 2 onload_amd/liboo_gpu_rx.so build/check/liboo_gpu_rx_r8e2.so build/check/liboo_gpu_rx_r6e4.so
   ;;
 u)  # per-group job sequences (OO_RX_GSEQ): parity of the variant, then A/B
-  for v in gseq gseql; do
+  for v in gseq; do
     OO_RX_LIB=build/var_$v.so timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py \
       tests/test_gpu_tx.py tests/test_gpu_l4_ref.py tests/test_gpu_xdp.py -x -q -p no:cacheprovider \
       --timeout 300 --timeout-method thread > "$OUT/${v}_parity.log" 2>&1
     rc=$?; echo "$v parity:"; tail -2 "$OUT/${v}_parity.log"; if [ $rc -ne 0 ]; then exit $rc; fi
   done
-  ab 2 "4 5 2" onload_amd/liboo_gpu_rx.so build/var_gseq.so build/var_gseql.so
+  ab 4 2 onload_amd/liboo_gpu_rx.so build/var_gseq.so
+  ab 2 "4 5" onload_amd/liboo_gpu_rx.so build/var_gseq.so
   ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
