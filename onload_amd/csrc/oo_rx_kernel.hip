@@ -1307,16 +1307,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v, uint32_t lane) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0xb1, 0xf, 0xf, false));   // [1,0,3,2]
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0x4e, 0xf, 0xf, false));   // [2,3,0,1]
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0x141, 0xf, 0xf, false));  // half mirror
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
-  v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401f));  // lane ^ 16
-  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // lane ^ 32
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)min((uint32_t)p[0], (uint32_t)p[1]));
-}
-
 // Rank of each lane's key among the wave's, largest first, ties in lane
 // order (a stable LSD radix sort on ballots; `bits` wave-uniform).
 __device__ __forceinline__ uint32_t rank_desc(uint32_t key, uint32_t lane, int bits) {
@@ -1404,7 +1394,6 @@ constexpr uint32_t NOJOB = 0xffffffffu;  // "no job": a round never reached
 // vector compare more than the lockstep slots.
 struct IssueCursor {
   uint32_t k;       // rounds issued (wave-uniform)
-  uint32_t knext;   // the first kend over the groups (wave-uniform)
   uint32_t js;      // the group's job position
   uint32_t kend;    // k at which the group's job ends (NOJOB: none)
   uint32_t kadv;    // k after which a stops advancing
@@ -1431,7 +1420,6 @@ __device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32
                                            uint32_t lane, uint64_t zero) {
   c.k = 0;
   issue_job(c, J, js, lane, zero);
-  c.knext = wave_min(c.kend);
 }
 
 // Issues the cursor's round into `slot`; groups whose job ends move on.
@@ -1439,8 +1427,9 @@ __device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint6
                                             void* slot, uint32_t lane) {
   glds<OO_RX_BODY_AUX>(c.a, slot);
   c.a += c.k < c.kadv ? 128u : 0u;
-  if (++c.k == c.knext) {  // some group's job ends (a scalar test per round)
-    const bool sw = c.k == c.kend;
+  ++c.k;
+  const bool sw = c.k == c.kend;
+  if (__ballot(sw) != 0) {  // some group's job ends
     IssueCursor n;
     n.k = c.k;
     issue_job(n, J, c.js + 1u, lane, zero);
@@ -1450,13 +1439,11 @@ __device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint6
       c.kadv = n.kadv;
       c.a = n.a;
     }
-    c.knext = wave_min(c.kend);
   }
 }
 
 struct ConsumeCursor {
   uint32_t k;           // rounds consumed (wave-uniform)
-  uint32_t knext;       // the first kend over the groups (wave-uniform)
   uint32_t js, kend;    // per group, as IssueCursor
   uint32_t klv;         // k up to which this lane has chunks of the job
   uint32_t vb;          // bytes of its last chunk in the frame (1..16)
@@ -1486,7 +1473,6 @@ __device__ __forceinline__ void consume_job(ConsumeCursor& c, const Jobs& J, uin
 __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, uint32_t lane) {
   c.k = 0;
   consume_job(c, J, 0, lane);
-  c.knext = wave_min(c.kend);
   c.acc = 0;
   c.bs = 0;
 }
@@ -1514,8 +1500,9 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
     b = dot(v.w & mm.w, 0x00010001u, b);
     c.acc = a + b;
   }
-  if (++c.k == c.knext) {  // some group's job ends (a scalar test per round)
-    const bool end = c.k == c.kend;
+  ++c.k;
+  const bool end = c.k == c.kend;
+  if (__ballot(end) != 0) {  // some group's job ends
     const uint32_t t = group_sum8(c.acc);
     ConsumeCursor n;
     n.k = c.k;
@@ -1529,7 +1516,6 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
       c.vb = n.vb;
       c.m = n.m;
     }
-    c.knext = wave_min(c.kend);
   }
 }
 #else
