@@ -191,7 +191,7 @@ struct oo_gpu_rx_ctx {
   int stage_next = 0;
   Tracked track[NTRACK];
   uint64_t lru = 0;
-  uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros + the sink
+  uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros, the sink, the hwport table
   uint32_t* d_claim = nullptr; // CLAIM_SETS x CLAIM_GROUPS counters, 128 B apart
   bool failed = false;         // a table flush failed part-way: the device copy is unknown
   bool dyn = true;             // dynamic tile claims (OO_RX_STATIC=1: static)
@@ -792,11 +792,14 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       hipMalloc(&T.occ6, sizeof(uint32_t) * ((n6 + 31) / 32)) == hipSuccess &&
       hipMalloc(&T.socks, sizeof(oo_gpu_rx_sock) * c->max_socks) == hipSuccess &&
       hipMalloc(&T.sockgen, sizeof(uint32_t) * c->max_socks) == hipSuccess &&
-      hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + 64u * 32u) == hipSuccess &&
+      hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + oo_rx::SINK_BYTES + OO_GPU_RX_MAX_INTF) ==
+          hipSuccess &&
       hipMalloc(&c->d_claim, 128u * CLAIM_SETS * CLAIM_GROUPS) == hipSuccess &&
       hipMemsetAsync(c->d_claim, 0, 128u * CLAIM_SETS * CLAIM_GROUPS, c->stream) == hipSuccess &&
       hipHostMalloc(&c->h_image_hdr, sizeof(ImageHdr), hipHostMallocDefault) == hipSuccess &&
       hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
+      hipMemcpyAsync(c->d_zero + 16u * oo_rx::ZERO_LINES + oo_rx::SINK_BYTES, c->hwport,
+                     OO_GPU_RX_MAX_INTF, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
       oo_table_launch_init(&T, c->stream) == 0;
   for (OpStage& st : c->stage)
     ok = ok && hipHostMalloc(&st.h, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK,
@@ -1055,7 +1058,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.zero = c->d_zero;
   P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
   P.stamps = c->stamps;
-  memcpy(P.hwport, c->hwport, sizeof(P.hwport));
+  P.hwport = c->d_zero + 16u * oo_rx::ZERO_LINES + oo_rx::SINK_BYTES;
   // Short frames (under 1 KiB of buffer per packet) are bound by the per-tile
   // header and table-lookup chain, not by the body stream: they take the
   // 2-slot-ring rx_kernel, whose smaller LDS footprint fits 12 waves per CU

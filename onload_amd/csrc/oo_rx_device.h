@@ -135,8 +135,10 @@ struct DevTables {
 };
 
 // The zero region read by lanes that have no chunk to load (64 KiB, so
-// those reads spread over the L2 channels).
+// those reads spread over the L2 channels).  The same allocation holds the
+// sink (64 x 32 B) and the context's intf_i_to_hwport table after it.
 constexpr uint32_t ZERO_LINES = 4096;
+constexpr uint32_t SINK_BYTES = 64u * 32u;
 
 // Wave groups of a launch at most: each has a tile-claim counter on a
 // 128-B line of its own (KParams::claim).
@@ -172,7 +174,7 @@ struct KParams {
   uint32_t ngroups;      // wave groups (a power of two, ngroups << gshift <= waves)
   uint32_t gshift;       // wave gwave is in group (gwave >> gshift) mod ngroups
   uint32_t dyn;          // 1: tiles past a wave's first three are claimed
-  uint8_t hwport[OO_GPU_RX_MAX_INTF];
+  const uint8_t* hwport;  // intf_i_to_hwport, OO_GPU_RX_MAX_INTF bytes in device memory
 };
 
 }  // namespace oo_rx

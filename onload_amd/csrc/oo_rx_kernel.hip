@@ -325,10 +325,10 @@ __device__ __forceinline__ Probe probe_of(const KParams& P, bool is6) {
 // issuing the next (six memory latencies instead of one).  The wait is
 // vmcnt(0): loads complete in issue order and these are the newest, so it
 // waits for nothing they would not.
-// With them, the lane's byte of the kernel arguments' intf_i_to_hwport
-// table at address ha (netif_table.h:33; a per-lane index, so a vector load,
-// which here costs no wait of its own -- inside the walks its wait would
-// drain the body stream).
+// With them, the lane's byte of the context's intf_i_to_hwport table at
+// address ha (netif_table.h:33, in HBM beside the zero region; a per-lane
+// index, so a vector load, which here costs no wait of its own -- inside the
+// walks its wait would drain the body stream).
 __device__ __forceinline__ void occ_words6(const Probe& t, const uint32_t i[6], uint32_t w[6],
                                            uint64_t ha, uint32_t& hw) {
   uint64_t a[6];
@@ -1122,9 +1122,7 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     // (intf_i_to_hwport for a valid interface; lanes with none read entry 0
     // and take 0xff)
     const bool intf_ok = (uint32_t)intf_i < (uint32_t)OO_GPU_RX_MAX_INTF;
-    // (the kernel's one argument, KParams, starts the argument segment)
-    const uint64_t hwa = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) +
-                         offsetof(KParams, hwport) + (intf_ok ? (uint32_t)intf_i : 0u);
+    const uint64_t hwa = sreg64(P.hwport) + (intf_ok ? (uint32_t)intf_i : 0u);
     uint32_t hwp = 0xffu;
     const bool tcp = proto == 6u;
     const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & t.mask;
