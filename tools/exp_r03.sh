@@ -247,6 +247,23 @@ u)  # per-group job sequences (OO_RX_GSEQ): parity of the variant, then A/B
   ab 4 2 onload_amd/liboo_gpu_rx.so build/var_gseq.so
   ab 2 "4 5" onload_amd/liboo_gpu_rx.so build/var_gseq.so
   ;;
+v)  # smoke(); the N>1 bench flow rehearsed on one GPU (two ranks sharing it over gloo)
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step rehearsal 600 env OO_BENCH_SHARE_GPU=1 OO_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 10 --warmup 3 \
+    --steady 20 > "$OUT/rehearsal_2ranks.json" 2> "$OUT/rehearsal_2ranks.err"
+  cat "$OUT/rehearsal_2ranks.json"
+  ;;
+w)  # the tile iteration as a template: lockstep only (d0) and per tile (d2) vs HEAD (ref)
+  for v in d0 d2; do
+    OO_RX_LIB=build/var_$v.so timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py \
+      tests/test_gpu_tx.py tests/test_gpu_l4_ref.py tests/test_gpu_xdp.py -x -q -p no:cacheprovider \
+      --timeout 300 --timeout-method thread > "$OUT/${v}_parity.log" 2>&1
+    rc=$?; echo "$v parity:"; tail -2 "$OUT/${v}_parity.log"; if [ $rc -ne 0 ]; then exit $rc; fi
+  done
+  ab 4 2 build/var_ref.so build/var_d0.so build/var_d2.so
+  ab 2 "4 5" build/var_ref.so build/var_d0.so build/var_d2.so
+  ab 1 3 build/var_ref.so build/var_d0.so build/var_d2.so
+  ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
   for r in 1 2; do
