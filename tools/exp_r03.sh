@@ -264,6 +264,17 @@ w)  # the tile iteration as a template: lockstep only (d0) and per tile (d2) vs 
   ab 2 "4 5" build/var_ref.so build/var_d0.so build/var_d2.so
   ab 1 3 build/var_ref.so build/var_d0.so build/var_d2.so
   ;;
+x)  # per-launch clock of the streaming probe alone (is the clock dip the workload's or the GPU's?)
+  (cd /tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d "$ROOT/$OUT/clk_probe" \
+     -o run --output-format csv -- "$ROOT/tools/ring_probe" 1610612736 c > "$ROOT/$OUT/clk_probe.log" 2>&1) \
+     || { echo "pmc clk_probe failed"; tail -3 "$OUT/clk_probe.log"; exit 1; }
+  grep -h '"tag"' "$OUT/clk_probe.log"
+  ;;
+y)  # the short-frame instance with per-group job sequences (product) vs HEAD (ref): parity, then A/B
+  tests
+  ab 3 "5 3" onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ab 1 "2 4" onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
   for r in 1 2; do

@@ -326,6 +326,24 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 2 && argv[2][0] == 'c') {  // 60 back-to-back launches (per-launch clock under rocprofv3)
+    const size_t nframes = (bytes - 4096) / 1536 / 64 * 64;
+    const int grid = cu * 10;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(e0, 0);
+    for (int r = 0; r < 60; ++r)
+      hipLaunchKernelGGL((ring_split<4, true, 1>), dim3(grid), dim3(64), (size_t)(4 + 8) * 1024, 0, a,
+                         nframes, o);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("{\"tag\":\"records_60_launches\",\"ms_per_launch\":%.4f}\n", ms / 60);
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'h') {  // one variant per run, for rocprofv3 --pmc
     if (argv[2][1] == '1') run_split<4, true, 0, 0, 1>(a, bytes, o, cu, "reads_half_body_lines");
     else run_split<4, true, 0>(a, bytes, o, cu, "reads");
