@@ -41,7 +41,7 @@ ab() {  # reps, configs, libs...
           > "$OUT/ab_last.json" 2> "$OUT/ab_last.err"
         rc=$?
         if [ $rc -ne 0 ]; then echo "$spec c$c rc=$rc"; tail -5 "$OUT/ab_last.err"; exit $rc; fi
-        echo "rep$rep c$c $spec $(python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); r=d["roofline"]; print(r["kernel_ms"], r["frac"], d["value"])' "$OUT/ab_last.json")" | tee -a "$OUT/ab.log"
+        echo "rep$rep c$c $spec $(python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); r=d["roofline"]; print(r["kernel_ms"], r["frac"], d["value"], "steady", (d.get("steady") or {}).get("kernel_ms"))' "$OUT/ab_last.json")" | tee -a "$OUT/ab.log"
       done
     done
   done
@@ -274,6 +274,9 @@ y)  # the short-frame instance with per-group job sequences (product) vs HEAD (r
   tests
   ab 3 "5 3" onload_amd/liboo_gpu_rx.so build/var_ref.so
   ab 1 "2 4" onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ;;
+z)  # ablation: the ring loop without its per-lane bookkeeping (results wrong), timed window and settled
+  ab 3 2 onload_amd/liboo_gpu_rx.so build/var_lean.so
   ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
