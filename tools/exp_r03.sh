@@ -278,6 +278,17 @@ y)  # the short-frame instance with per-group job sequences (product) vs HEAD (r
 z)  # ablation: the ring loop without its per-lane bookkeeping (results wrong), timed window and settled
   ab 3 2 onload_amd/liboo_gpu_rx.so build/var_lean.so
   ;;
+fa)  # wave-uniform fast path for the body rounds (product) vs HEAD (ref): full suite, then A/B
+  tests
+  ab 4 2 onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ab 2 4 onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ab 1 5 onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ;;
+fb)  # group 0's slot job by readlane instead of three bpermutes (product) vs HEAD (ref)
+  tests
+  ab 4 2 onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ab 1 "4 5" onload_amd/liboo_gpu_rx.so build/var_ref.so
+  ;;
 final)  # the round's evidence: full GPU suite, driver-shaped bench lines, rocprof of the same command
   tests
   for r in 1 2; do
