@@ -36,6 +36,12 @@ extern "C" int oo_rx_blocks_per_cu(void);
 extern "C" int oo_rx_launch_short(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_rx_blocks_per_cu_short(void);
 extern "C" int oo_rx_waves_per_block(void);
+extern "C" int oo_rx_win_blocks_per_cu(void);
+extern "C" int oo_rx_body_blocks_per_cu(void);
+extern "C" int oo_rx_win_waves_per_block(void);
+extern "C" int oo_rx_body_waves_per_block(void);
+extern "C" int oo_rx_launch_win(const oo_rx::KParams* P, int grid, hipStream_t stream);
+extern "C" int oo_rx_launch_body(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
                                    const uint32_t* d_lev_end, uint32_t nlev, uint32_t gen,
                                    hipStream_t s);
@@ -100,7 +106,8 @@ constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 K
 constexpr int NTRACK = 8;             // streams tracked at once (LRU)
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
 // Tile-claim counter sets: two per tracked stream (its launches alternate
-// between them), oo_rx::CLAIM_GROUPS counters of 128 B each.
+// between them), oo_rx::CLAIM_LINES lines of 128 B each (both kernels' group
+// counters and the body flag).
 constexpr uint32_t CLAIM_SETS = 2 * NTRACK;
 using oo_rx::CLAIM_GROUPS;
 
@@ -121,6 +128,8 @@ struct Tracked {
   uint32_t parity = 0;    // claim set of the next launch (of the entry's two)
   uint32_t tables_seen = 0;  // table generation this stream has waited for
   uint64_t lru = 0;
+  uint64_t* pend = nullptr;  // the split transform's pending words (launch_split)
+  uint64_t pend_n = 0;
 };
 
 // One op-flush staging buffer: pinned host ops -> device ops, reused once
@@ -192,7 +201,7 @@ struct oo_gpu_rx_ctx {
   Tracked track[NTRACK];
   uint64_t lru = 0;
   uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros, the sink, the hwport table
-  uint32_t* d_claim = nullptr; // CLAIM_SETS x CLAIM_GROUPS counters, 128 B apart
+  uint32_t* d_claim = nullptr; // CLAIM_SETS x CLAIM_LINES words, 128 B apart
   bool failed = false;         // a table flush failed part-way: the device copy is unknown
   bool dyn = true;             // dynamic tile claims (OO_RX_STATIC=1: static)
   uint32_t tail_tile = 32;     // packets per tile at the batch's end (dynamic)
@@ -201,6 +210,9 @@ struct oo_gpu_rx_ctx {
   uint32_t gshift = ~0u;       // claim group of a wave: (gwave >> gshift) mod groups (~0u: per launch)
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t grid_short = 0;     // resident blocks of the short-frame rx_kernel (0: unused)
+  uint32_t grid_win = 0;       // resident blocks of win_kernel (split transform)
+  uint32_t grid_body = 0;      // resident blocks of body_kernel
+  uint32_t body_tail = 16;     // packets per body_kernel unit at the batch's end
   uint32_t kmode = 0;          // rx kernel: 0 by frame size, 1 always the 4-slot, 2 always the 2-slot
   uint32_t len_hint = 0;       // mean frame length of the batches to come (0: from buffer bytes)
   uint32_t tstep = 8;          // tile size step (KParams::tstep)
@@ -536,8 +548,10 @@ void free_dev(oo_gpu_rx_ctx* c) {
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
-  for (Tracked& t : c->track)
+  for (Tracked& t : c->track) {
     if (t.ev) (void)hipEventDestroy(t.ev);
+    if (t.pend) (void)hipFree(t.pend);
+  }
   for (const HostReg& r : c->regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.lo));
   if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
   if (c->h_image_hdr) (void)hipHostFree(c->h_image_hdr);
@@ -769,11 +783,17 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
     const int b1 = oo_rx_blocks_per_cu_short();
     if (b1 > 0)
       c->grid_short = std::max<uint32_t>(1, (uint32_t)(b1 * prop.multiProcessorCount) * pct / 100);
+    const int bw = oo_rx_win_blocks_per_cu();
+    if (bw > 0) c->grid_win = (uint32_t)(bw * prop.multiProcessorCount);
+    const uint32_t bb = std::min<uint32_t>((uint32_t)std::max(0, oo_rx_body_blocks_per_cu()),
+                                           env_u32("OO_RX_BODY_BPC", 64));
+    if (bb > 0) c->grid_body = bb * (uint32_t)prop.multiProcessorCount;
   }
   c->tstep = env_u32("OO_RX_TSTEP", 8) == 1 ? 1 : 8;
   c->dyn = env_u32("OO_RX_STATIC", 0) == 0;
   c->tail_tile = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_TAIL_TILE", 32) / 8 * 8));
   c->tail_per_wave = env_u32("OO_RX_TAIL_PER_WAVE", 1);
+  c->body_tail = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_BODY_TAIL", 16) / 8 * 8));
   c->kmode = env_u32("OO_RX_KERNEL", 0);
   c->ngroups_max = std::min<uint32_t>(CLAIM_GROUPS, env_u32("OO_RX_GROUPS", 0));  // 0: by frame size
   c->gshift = env_u32("OO_RX_GSHIFT", ~0u);                                       // ~0: by frame size
@@ -794,8 +814,8 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       hipMalloc(&T.sockgen, sizeof(uint32_t) * c->max_socks) == hipSuccess &&
       hipMalloc(&c->d_zero, 16u * oo_rx::ZERO_LINES + oo_rx::SINK_BYTES + OO_GPU_RX_MAX_INTF) ==
           hipSuccess &&
-      hipMalloc(&c->d_claim, 128u * CLAIM_SETS * CLAIM_GROUPS) == hipSuccess &&
-      hipMemsetAsync(c->d_claim, 0, 128u * CLAIM_SETS * CLAIM_GROUPS, c->stream) == hipSuccess &&
+      hipMalloc(&c->d_claim, 128u * CLAIM_SETS * oo_rx::CLAIM_LINES) == hipSuccess &&
+      hipMemsetAsync(c->d_claim, 0, 128u * CLAIM_SETS * oo_rx::CLAIM_LINES, c->stream) == hipSuccess &&
       hipHostMalloc(&c->h_image_hdr, sizeof(ImageHdr), hipHostMallocDefault) == hipSuccess &&
       hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
       hipMemcpyAsync(c->d_zero + 16u * oo_rx::ZERO_LINES + oo_rx::SINK_BYTES, c->hwport,
@@ -1027,6 +1047,74 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, vo
   return 0;
 }
 
+// A launch's claim groups: the largest power of two <= gmax with ngroups
+// << gshift <= W (every group has a wave).
+static void set_groups(KParams& P, uint64_t W, uint32_t gmax, uint32_t gshift) {
+  P.gshift = std::min<uint32_t>(gshift, 16u);
+  while (P.gshift > 0 && (1ull << P.gshift) > W) --P.gshift;
+  P.ngroups = 1;
+  while (P.ngroups < gmax && (2ull * P.ngroups << P.gshift) <= W) P.ngroups *= 2;
+}
+
+// Dynamic partition of n packets for W waves: full 64-packet tiles, then
+// about per_wave tiles of S packets per wave (the last taking what is left,
+// at least one packet), so the waves that finish early take the small tiles
+// and all end within a small tile of each other.
+static void set_tiles_dyn(KParams& P, uint32_t n, uint64_t W, uint32_t S, uint32_t per_wave) {
+  const uint64_t tail = W * per_wave * S;
+  const uint64_t NA = n > tail ? (n - tail) / 64 : 0;
+  const uint64_t NS = S < 64 ? (n - 64 * NA + S - 1) / S : 0;
+  P.ntiles = (uint32_t)(NA + NS);
+  P.tlo = S;
+  P.tstep = 64 - S;
+  P.ta = (uint32_t)NA;
+  if (S == 64) {  // no tail: plain 64-packet tiles
+    P.ntiles = (n + 63) / 64;
+    P.tlo = 64;
+    P.tstep = 0;
+    P.ta = 0;
+  }
+}
+
+// The split transform (oo_rx_kernel.hip "The split transform"): win_kernel,
+// then body_kernel, on s.  The stream's pending-word buffer grows in stream
+// order (hipMallocAsync), so no call waits for the device.
+static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Tracked* trk,
+                        uint32_t* set, hipStream_t s) {
+  if (trk->pend_n < (uint64_t)n + 64) {
+    if (trk->pend != nullptr && hipFreeAsync(trk->pend, s) != hipSuccess) return -EIO;
+    trk->pend = nullptr;
+    trk->pend_n = 0;
+    const uint64_t want = std::max<uint64_t>((uint64_t)n + 64, 1u << 16);
+    if (hipMallocAsync(reinterpret_cast<void**>(&trk->pend), want * 8, s) != hipSuccess) return -ENOMEM;
+    trk->pend_n = want;
+  }
+  KParams B = base, A = base;
+  B.pend = A.pend = trk->pend;
+  B.flag = A.flag = set + 32u * oo_rx::FLAG_LINE;
+  // win_kernel: header-bound tiles, many claims per us (32 groups of
+  // 16-wave runs, each over all eight XCDs).
+  const uint64_t WB = (uint64_t)c->grid_win * (uint32_t)oo_rx_win_waves_per_block();
+  const uint32_t blocks_b =
+      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + 1) / 2, c->grid_win));
+  const uint64_t WBl = (uint64_t)blocks_b * (uint32_t)oo_rx_win_waves_per_block();
+  (void)WB;
+  set_groups(B, WBl, 32u, 4u);
+  set_tiles_dyn(B, n, WBl, c->tail_tile, c->tail_per_wave);
+  // body_kernel: stream-bound units (64 single-wave groups), a finer tail.
+  const uint32_t blocks_a =
+      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + 1) / 2, c->grid_body));
+  const uint64_t WA = (uint64_t)blocks_a * (uint32_t)oo_rx_body_waves_per_block();
+  A.claim = set + 32u * CLAIM_GROUPS;
+  A.claim_next = nullptr;
+  set_groups(A, WA, CLAIM_GROUPS, 0u);
+  set_tiles_dyn(A, n, WA, c->body_tail, 1);
+  A.dyn = B.dyn = 1u;
+  if (oo_rx_launch_win(&B, (int)blocks_b, s) != 0) return -EIO;
+  if (oo_rx_launch_body(&A, (int)blocks_a, s) != 0) return -EIO;
+  return 0;
+}
+
 // tx: the TX checksum fill (tx_kernel) instead of the RX transform.
 static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
                   const oo_gpu_pkt_desc* d_desc, uint32_t n, oo_gpu_rx_result* d_out,
@@ -1069,6 +1157,20 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // per packet (a packed batch).
   const bool short_frames =
       c->len_hint ? c->len_hint < 1024u : P.frames_bytes < 1024ull * n;
+  // The stream's own claim counter sets (Tracked): launches on one stream
+  // run in order and alternate between the two; each zeroes the other.
+  Tracked* trk = track_of(c, s);
+  if (trk == nullptr) return -EIO;
+  uint32_t* const sets = c->d_claim + 2u * 32u * oo_rx::CLAIM_LINES * track_index(c, trk);
+  P.claim = sets + 32u * oo_rx::CLAIM_LINES * trk->parity;
+  P.claim_next = sets + 32u * oo_rx::CLAIM_LINES * (trk->parity ^ 1u);
+  if (!tx && c->kmode == 0 && c->grid_win > 0 && c->grid_body > 0) {
+    const int rc = launch_split(c, P, n, trk, P.claim, s);
+    if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
+    trk->parity ^= 1u;
+    note_launch(trk);
+    return 0;
+  }
   const bool use_short = !tx && c->grid_short > 0 && (c->kmode == 2 || (c->kmode == 0 && short_frames));
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
   const uint32_t need = (n + 63) / 64;  // waves if every tile were full
@@ -1076,43 +1178,15 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
       1, std::min<uint32_t>((need + wpb - 1) / wpb, use_short ? c->grid_short : c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
   // The launch's claim counters (zeroed by the stream's previous launch),
-  // one per wave group: the largest power of two <= the group limit with
-  // ngroups << gshift <= W (every group has a wave).  Short frames (under
-  // 1 KiB of buffer per packet: header-bound tiles, many claims per us) use
-  // 32 groups of eight-block runs, each group spread over all eight XCDs;
-  // long frames 64 groups of single waves (same-box A/B).
-  // The stream's own claim counter sets (Tracked): launches on one stream
-  // run in order and alternate between the two.
-  Tracked* trk = track_of(c, s);
-  if (trk == nullptr) return -EIO;
-  uint32_t* const sets = c->d_claim + 2u * 32u * CLAIM_GROUPS * track_index(c, trk);
-  P.claim = sets + 32u * CLAIM_GROUPS * trk->parity;
-  P.claim_next = sets + 32u * CLAIM_GROUPS * (trk->parity ^ 1u);
-  uint32_t gmax = c->ngroups_max ? c->ngroups_max : (short_frames ? 32u : CLAIM_GROUPS);
-  P.gshift = std::min<uint32_t>(c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u), 16u);
-  while (P.gshift > 0 && (1ull << P.gshift) > W) --P.gshift;
-  P.ngroups = 1;
-  while (P.ngroups < gmax && (2ull * P.ngroups << P.gshift) <= W) P.ngroups *= 2;
+  // one per wave group.  Short frames (under 1 KiB of buffer per packet:
+  // header-bound tiles, many claims per us) use 32 groups of eight-block
+  // runs, each group spread over all eight XCDs; long frames 64 groups of
+  // single waves (same-box A/B).
+  set_groups(P, W, c->ngroups_max ? c->ngroups_max : (short_frames ? 32u : CLAIM_GROUPS),
+             c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u));
   P.dyn = c->dyn ? 1u : 0u;
   if (c->dyn) {
-    // Dynamic: full 64-packet tiles, then about tail_per_wave tiles of
-    // tail_tile packets per wave (the last taking what is left, at least
-    // one packet), so the waves that finish early take the small tiles and
-    // all end within a small tile of each other.
-    const uint64_t S = c->tail_tile;
-    const uint64_t tail = W * c->tail_per_wave * S;
-    const uint64_t NA = n > tail ? (n - tail) / 64 : 0;
-    const uint64_t NS = S < 64 ? (n - 64 * NA + S - 1) / S : 0;
-    P.ntiles = (uint32_t)(NA + NS);
-    P.tlo = (uint32_t)S;
-    P.tstep = (uint32_t)(64 - S);
-    P.ta = (uint32_t)NA;
-    if (S == 64) {  // no tail: plain 64-packet tiles
-      P.ntiles = (uint32_t)((n + 63) / 64);
-      P.tlo = 64;
-      P.tstep = 0;
-      P.ta = 0;
-    }
+    set_tiles_dyn(P, n, W, c->tail_tile, c->tail_per_wave);
   } else {
     // Static balanced partition: the W waves each take K = ceil(n / (64 W))
     // tiles; NT = W K tiles of tlo or tlo + 8 packets (multiples of 8, at

@@ -143,6 +143,20 @@ constexpr uint32_t SINK_BYTES = 64u * 32u;
 // Wave groups of a launch at most: each has a tile-claim counter on a
 // 128-B line of its own (KParams::claim).
 constexpr uint32_t CLAIM_GROUPS = 64;
+// One claim set: the window (or tile) kernel's group counters, the body
+// kernel's group counters, and the body flag, each on a 128-B line.
+constexpr uint32_t CLAIM_LINES = 2 * CLAIM_GROUPS + 1;
+constexpr uint32_t FLAG_LINE = 2 * CLAIM_GROUPS;
+
+// The split transform's pending word of a frame with a body (KParams::pend,
+// 8 B per packet, written by win_kernel, read by body_kernel):
+//  bits  0-15  the body-sum residue mod 0xffff for which the L4 checksum
+//              passes; PEND_NONE: the verdict does not wait for the body
+//  bit  16     TCP (else UDP)
+//  bits 17-18  the record's OO_RX_F_IP6 / OO_RX_F_VLAN flags
+//  bits 24-28  the record's reason as written (the sum passing)
+//  bits 32-47  vlan, 48-63 ip_paylen (the drop record keeps them)
+constexpr uint32_t PEND_NONE = 0xffffu;
 
 // Kernel arguments (passed by value).
 struct KParams {
@@ -175,6 +189,8 @@ struct KParams {
   uint32_t gshift;       // wave gwave is in group (gwave >> gshift) mod ngroups
   uint32_t dyn;          // 1: tiles past a wave's first three are claimed
   const uint8_t* hwport;  // intf_i_to_hwport, OO_GPU_RX_MAX_INTF bytes in device memory
+  uint64_t* pend;        // split transform: a pending word per packet (n + 64 entries)
+  uint32_t* flag;        // split transform: non-zero once a verdict waits for a body
 };
 
 }  // namespace oo_rx

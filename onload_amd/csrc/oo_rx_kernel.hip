@@ -2125,6 +2125,19 @@ __device__ __forceinline__ void claim_tile(uint32_t* ctr, uint32_t step, uint32_
   if (lane == 0) got = __hip_atomic_fetch_add(ctr, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Zeroes the claim set the stream's next launch uses (its CLAIM_LINES lines:
+// both kernels' group counters and the body flag) with three `sc1` stores;
+// the launch before it, the last to use that set, has finished (stream
+// order).
+__device__ __forceinline__ void zero_claim_set(uint32_t* set, uint32_t lane) {
+  static_assert(CLAIM_GROUPS == 64, "one lane per group counter");
+  __hip_atomic_store(set + 32u * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(set + 32u * (CLAIM_GROUPS + lane), 0u, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0)
+    __hip_atomic_store(set + 32u * FLAG_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The claim group of wave gwave: runs of B = 2^gshift consecutive waves
 // (gshift 4: eight blocks, one on each XCD) dealt round-robin to the groups.
 __device__ __forceinline__ uint32_t group_of(const KParams& P, uint32_t gwave) {
@@ -2150,9 +2163,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   // zeroes the set the next one will use (the launch before it, which left
   // that set's counters where its claims ended, has finished: stream order).
   // No wave has to wait for the others' claims at the end.
-  static_assert(CLAIM_GROUPS == 64, "one lane per group counter");
-  if (gwave == 0)
-    __hip_atomic_store(P.claim_next + 32u * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (gwave == 0) zero_claim_set(P.claim_next, lane);
   // Tiles i, i + 1, i + 2 of this wave, and the claim of tile i + 3.
   uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
   uint32_t claimed = 0;  // the last claim, once read (have)
@@ -2399,6 +2410,344 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void tx_kernel(KParams P) {
   tile_loop<true>(P);
 }
+
+// ===========================================================================
+// The split transform (DESIGN.md §2 "Two launches"): a batch is two
+// launches on its stream.
+//  win_kernel   the header work of every packet -- descriptor, window
+//               staging, parse, demux -- and every record, final unless the
+//               L4 verdict waits for the frame's body (then written as if
+//               the body sum passes); for the tiles holding frames with a
+//               body, one 8-B pending word per packet (KParams::pend).
+//  body_kernel  the bodies of the frames whose verdict waits, streamed by
+//               the body engine above with nothing else in the wave's memory
+//               queue; a frame whose sum fails gets the drop record that
+//               finish() would have written.
+// The records (2 % of config 2's bytes) are then written in win_kernel's
+// short launch instead of between the body stream's reads: HBM pays for
+// interleaved writes about a tenth of the stream's time.
+
+// The body residue mod M = 0xffff for which the L4 verdict passes.  finish()
+// passes iff fold16(f + pseudo) == 0xffff with f = fold16(s4 + body),
+// byte-swapped for an odd frame address; a byte swap multiplies by 2^8 mod M
+// and fold16 keeps the residue, so (pseudo >= 1: the sum is never 0) that is
+// sigma (s4 + body) + pseudo == 0 (mod M), sigma = 256 or 1, i.e. body ==
+// -s4 - sigma pseudo (mod M) (sigma^2 == 1 mod M).  s4 is the window part
+// as the parse leaves it, possibly negative ("Why the split sum is exact";
+// |s4| < 2^31: at most a 64-KiB frame's words).
+__device__ __forceinline__ uint32_t res16(uint32_t x) {  // x mod 0xffff
+  const uint32_t f = fold16(x);
+  return f == 0xffffu ? 0u : f;
+}
+__device__ __forceinline__ uint32_t body_target(uint32_t s4, uint32_t pseudo, bool odd) {
+  const int32_t sv = (int32_t)s4;
+  const uint32_t r4 = sv >= 0 ? res16((uint32_t)sv) : (0xffffu - res16((uint32_t)(-(int64_t)sv))) % 0xffffu;
+  uint32_t rp = res16(pseudo);
+  if (odd) rp = res16(rp << 8);
+  return (2u * 0xffffu - r4 - rp) % 0xffffu;
+}
+
+constexpr int WAVES_W = 2;  // win_kernel: waves per block
+#ifndef OO_RX_WIN_WPE
+#define OO_RX_WIN_WPE 4  // win_kernel: waves per SIMD the register budget allows
+#endif
+
+struct WinLds {
+  uint4 hdr[HC][64];             // header windows (stage_window)
+  uint4 desc[2][64];             // descriptors of tile t (buffer t & 1) and t + 1
+  uint32_t cnt[OO_RX_R_COUNT];   // per-reason counts
+  uint32_t dbase, gofs, pad0, pad1;
+};
+static_assert(sizeof(WinLds) % 16 == 0, "WinLds is carved from a uint4 array");
+constexpr int WIN_U4 = (int)(sizeof(WinLds) / 16);
+
+// win_kernel's tile loop.  The same tiles, descriptor and window staging,
+// parse, demux and claims as tile_loop, without a body: while tile t's
+// lookups run, tile t+1's windows land (staged before the demux: its first
+// level's wait then also covers them, one latency for both), and the
+// descriptors of tile t+2 (into the buffer tile t's came in: read at the
+// tile's start).  Counted waits, as tile_loop ("rx_kernel" above): per tile
+// HC window rows, one descriptor line and the claim, then the demux loads
+// (each level ends in vmcnt(0)), then NST record stores, and -- only for
+// tiles holding a frame with a body -- the pending words and the body flag
+// (uncounted: an operation the count leaves out only makes a wait
+// stricter).
+__device__ __forceinline__ void window_loop(const KParams& P) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_W * WIN_U4];
+  const int wave = (int)(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  WinLds& L = reinterpret_cast<WinLds*>(smem)[wave];
+  const uint32_t gwave = sreg(blockIdx.x * WAVES_W + wave);
+  const uint32_t W = gridDim.x * WAVES_W;
+  if (gwave == 0) zero_claim_set(P.claim_next, lane);
+  uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
+  if (lane == 0) {
+    const uint32_t g = group_of(P, gwave);
+    lds_write4(&L.dbase, 3u * W + g);
+    lds_write4(&L.gofs, 32u * g);
+  }
+  if (gwave >= P.ntiles) return;
+  if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
+
+  // Prologue: tile t0's descriptors and windows, then t1's descriptors.
+  {
+    const Unit t0 = unit_of(P, tcur);
+    glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
+    vm_wait<0>();
+    const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
+    stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
+    glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
+  }
+
+  uint32_t b = 0;
+  for (uint32_t it_ = 0; tcur < P.ntiles; b ^= 1u, ++it_) {
+    const Unit tile = unit_of(P, tcur);
+    // This tile's windows (and its descriptors, older): newer are the next
+    // tile's descriptor line and, after the first tile, the claim and the
+    // previous tile's record stores.
+    if (it_ == 0) vm_wait<1>();
+    else vm_wait<2 + NST>();
+    const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), tile, lane);
+    const Hdr h = parse_headers(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
+
+    // ---- stage the next tile: its windows into the rows the parse has
+    // read (its descriptor line: newer are the claim and the record stores),
+    // the descriptors of the tile after it, the claim of the tile after that.
+    if (it_ != 0) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+      tnext2 = P.dyn ? sreg(lds_read4(&L.dbase)) + c : tnext2 + W;
+      vm_wait<1 + NST>();
+    } else {
+      vm_wait<0>();
+    }
+    {
+      const Unit nt = unit_of(P, tnext);
+      const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the parse's LDS reads are done
+      stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
+    }
+    glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
+    claim_tile(P.claim + sreg(lds_read4(&L.gofs)), P.ngroups, lane, got);
+
+    // ---- lookups and the record.
+    Parsed ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
+    if (P.counters != nullptr && dv.valid) lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
+    store_records(P, tile, ps.r, lane);
+    // The pending words of a tile holding frames with a body.
+    const bool body = dv.span > HB;
+    if (__ballot(body) != 0) {
+      const bool wait = (ps.odd_long & 2u) != 0;
+      const uint32_t tgt = wait ? body_target(ps.s4, ps.pseudo, (ps.odd_long & 1u) != 0) : PEND_NONE;
+      const uint32_t lo = tgt | (ps.r.proto == 6u ? 1u << 16 : 0u) |
+                          ((uint32_t)(ps.r.flags & (OO_RX_F_IP6 | OO_RX_F_VLAN)) << 17) |
+                          ((uint32_t)ps.r.reason << 24);
+      const uint32_t hi = (uint32_t)ps.r.vlan | ((uint32_t)ps.r.ip_paylen << 16);
+      if (lane < tile.cnt) P.pend[tile.first + lane] = (uint64_t)lo | ((uint64_t)hi << 32);
+      if (__ballot(wait) != 0 && lane == 0)
+        __hip_atomic_store(P.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    tcur = tnext;
+    tnext = tnext2;
+  }
+  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (P.counters != nullptr) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (ln < OO_RX_R_COUNT) {
+      const uint32_t c = lds_read4(&L.cnt[ln]);
+      if (c != 0) atomicAdd(&P.counters[ln], c);
+    }
+  }
+}
+
+__global__ __launch_bounds__(WAVES_W * 64) __attribute__((amdgpu_waves_per_eu(OO_RX_WIN_WPE))) void win_kernel(
+    KParams P) {
+  window_loop(P);
+}
+
+// ---------------------------------------------------------------------------
+// body_kernel: units of up to 64 packets (its own partition, finer at the
+// batch's end); per unit the packets whose pending word waits for the body
+// are the jobs of the body engine (lockstep slots, as tile_loop), an RB-slot
+// ring with nothing else in the wave's memory queue.  A slot's first F
+// rounds hold a whole chunk for every lane (F from the slot's smallest job),
+// so they take neither the per-lane live/partial tests nor the per-lane
+// advance test.
+#ifndef OO_RX_BODY_RING
+#define OO_RX_BODY_RING 8
+#endif
+constexpr int RB = OO_RX_BODY_RING;
+static_assert(RB % 2 == 0, "the ring is consumed two pieces at a time");
+constexpr int WAVES_B = 2;
+
+struct BodyLds {
+  uint4 ring[RB][64];
+  uint4 desc[2][64];             // descriptors of this unit and the next
+  uint32_t pend[2][2][64];       // their pending words (low, high halves)
+  uint32_t cnt[OO_RX_R_COUNT];   // per-reason count changes
+  uint32_t dbase, gofs, pad0, pad1;
+};
+static_assert(sizeof(BodyLds) % 16 == 0, "BodyLds is carved from a uint4 array");
+constexpr int BODY_U4 = (int)(sizeof(BodyLds) / 16);
+
+// min(v) over the lanes with the same lane & 7 (as max_x8).
+__device__ __forceinline__ uint32_t min_x8(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
+  v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401f));  // lane ^ 16
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // lane ^ 32
+  return min((uint32_t)p[0], (uint32_t)p[1]);
+}
+
+// The rounds of slot js in which every lane reads a whole chunk that is not
+// its job's last: its smallest job's (nb - 1) / 8 (0 when a group has none).
+// fm: min_x8 of the jobs' chunk counts (lane j: slot j's).
+__device__ __forceinline__ uint32_t slot_full(uint32_t fm, uint32_t js) {
+  const uint32_t m = js < 8u ? (uint32_t)__builtin_amdgcn_readlane((int)fm, (int)js) : 0u;
+  return m != 0 ? (m - 1u) >> 3 : 0u;
+}
+
+// The loads of a unit's descriptors and pending words into buffer b (three
+// operations).
+__device__ __forceinline__ void stage_unit(const KParams& P, const Unit& u, uint32_t lane,
+                                           BodyLds& L, uint32_t b) {
+  glds<0>(desc_src(P, u, lane), &L.desc[b][0]);
+  const uint32_t i = u.first + lane;  // in the padded pend array (n + 64 entries)
+  const uint64_t pa = reinterpret_cast<uint64_t>(P.pend) + 8ull * i;
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(pa), (lptr)(&L.pend[b][0][0]), 4, 0, 0);
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(pa + 4u), (lptr)(&L.pend[b][1][0]), 4, 0, 0);
+}
+
+__device__ __forceinline__ void body_loop(const KParams& P) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_B * BODY_U4];
+  const int wave = (int)(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  BodyLds& L = reinterpret_cast<BodyLds*>(smem)[wave];
+  const uint32_t gwave = sreg(blockIdx.x * WAVES_B + wave);
+  const uint32_t W = gridDim.x * WAVES_B;
+  // No frame of the batch waits for its body: nothing to do.
+  if (__hip_atomic_load(P.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  if (gwave >= P.ntiles) return;
+  uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
+  if (lane == 0) {
+    const uint32_t g = group_of(P, gwave);
+    lds_write4(&L.dbase, 3u * W + g);
+    lds_write4(&L.gofs, 32u * g);
+  }
+  if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
+  stage_unit(P, unit_of(P, tcur), lane, L, 0);
+  stage_unit(P, unit_of(P, tnext), lane, L, 1);
+  vm_wait<0>();
+
+  uint32_t b = 0;
+  for (uint32_t it_ = 0; tcur < P.ntiles; b ^= 1u, ++it_) {
+    const Unit unit = unit_of(P, tcur);
+    const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), unit, lane);
+    const uint32_t plo = lds_read4(&L.pend[b][0][lane]);
+    const uint32_t phi = lds_read4(&L.pend[b][1][lane]);
+    const uint64_t zero = zero_line(P, unit, lane);
+    // Jobs: the frames with a body whose verdict waits for it.
+    const uint32_t tgt = plo & 0xffffu;
+    const bool job = dv.valid && dv.span > HB && tgt != PEND_NONE;
+    uint32_t myslot;
+    const Jobs J = jobs_setup(dv.abase, job ? dv.span : 0, lane, myslot);
+    const uint32_t fm = min_x8(J.nb);
+
+    // ---- stage the unit after next (into this unit's buffers, now read)
+    // and claim the one after that: older than this unit's rounds, so the
+    // ring's waits need not count them.
+    if (it_ != 0) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+      tnext2 = P.dyn ? sreg(lds_read4(&L.dbase)) + c : tnext2 + W;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage_unit(P, unit_of(P, tnext2), lane, L, b);
+    claim_tile(P.claim + sreg(lds_read4(&L.gofs)), P.ngroups, lane, got);
+
+    const uint32_t T = (J.T + RB - 1) / RB * RB;
+    uint32_t bsum = 0;
+    if (T != 0) {
+      // issue side
+      IssueCursor ci;
+      issue_slot(ci, J, 0, lane, zero);
+      uint32_t fi = slot_full(fm, 0);
+      auto issue = [&](void* slot) {
+        glds<OO_RX_BODY_AUX>(ci.a, slot);
+        if (ci.rnd + 1u < fi) ci.a += 128u;  // every lane reads on (scalar test)
+        else ci.a += ci.rnd < ci.adv ? 128u : 0u;
+        if (++ci.rnd == ci.R) {
+          issue_slot(ci, J, ci.js + 1, lane, zero);
+          fi = slot_full(fm, ci.js);
+        }
+      };
+#pragma unroll
+      for (int u = 0; u < RB; ++u) issue(&L.ring[u][0]);
+      // consume side
+      ConsumeCursor cc;
+      consume_start(cc, J, lane);
+      uint32_t fc = slot_full(fm, 0);
+      auto consume = [&](const uint4& v) {
+        if (cc.rnd < fc) {  // every lane: a whole chunk, not its last
+          uint32_t a = dot(v.x, 0x00010001u, cc.acc);
+          uint32_t b2 = dot(v.y, 0x00010001u, 0u);
+          a = dot(v.z, 0x00010001u, a);
+          b2 = dot(v.w, 0x00010001u, b2);
+          cc.acc = a + b2;
+          ++cc.rnd;
+        } else {
+          consume_round(cc, J, v, lane);  // (it moves to the next slot itself)
+          if (cc.rnd == 0) fc = slot_full(fm, cc.js);
+        }
+      };
+      for (uint32_t k0 = 0; k0 < T; k0 += RB) {
+        const bool last = k0 + RB == T;
+#pragma unroll
+        for (int u = 0; u < RB; u += 2) {
+          if (last) vm_wait_n(RB - 2 - u);
+          else vm_wait<RB - 2>();
+          uint4 v0, v1;
+          lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
+          consume(v0);
+          consume(v1);
+          if (!last) {
+            issue(&L.ring[u][0]);
+            issue(&L.ring[u + 1][0]);
+          }
+        }
+      }
+      bsum = lane_get(cc.bs, myslot);
+    }
+
+    // ---- verdicts: a failing sum turns the record into the drop record.
+    const bool fail = job && res16(bsum) != tgt;
+    if (__ballot(fail) != 0) {
+      if (fail) {
+        const bool tcp = (plo >> 16) & 1u;
+        const uint32_t reason = tcp ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+        const uint4 r0 = make_uint4(reason | (((plo >> 17) & 3u) << 8) | ((tcp ? 6u : 17u) << 24),
+                                    phi & 0xffffu, phi >> 16, 0u);
+        const uint4 r1 = make_uint4(0u, 0u, 0xffffffffu, 0u);
+        uint4* const o = reinterpret_cast<uint4*>(P.out) + 2ull * dv.idx;
+        o[0] = r0;
+        o[1] = r1;
+        if (P.counters != nullptr) {
+          lds_add4(&L.cnt[(plo >> 24) & (OO_RX_R_COUNT - 1)], 0xffffffffu);
+          lds_add4(&L.cnt[reason], 1u);
+        }
+      }
+    }
+    tcur = tnext;
+    tnext = tnext2;
+  }
+  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (P.counters != nullptr) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (ln < OO_RX_R_COUNT) {
+      const uint32_t c = lds_read4(&L.cnt[ln]);
+      if (c != 0) atomicAdd(&P.counters[ln], c);
+    }
+  }
+}
+
+__global__ __launch_bounds__(WAVES_B * 64) void body_kernel(KParams P) { body_loop(P); }
 #endif
 
 }  // namespace oo_rx
@@ -2438,6 +2787,31 @@ extern "C" int oo_tx_launch(const oo_rx::KParams* P, int grid, hipStream_t strea
 // Launch one RX batch on `stream`.
 extern "C" int oo_rx_launch(const oo_rx::KParams* P, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(oo_rx::rx_kernel, dim3(grid), dim3(oo_rx::WAVES * 64), 0, stream, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The split transform's two kernels: resident blocks per CU, waves per
+// block, launches.
+extern "C" int oo_rx_win_blocks_per_cu(void) {
+  int b = 0;
+  const hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::win_kernel, oo_rx::WAVES_W * 64, 0);
+  return e == hipSuccess ? b : 0;
+}
+extern "C" int oo_rx_body_blocks_per_cu(void) {
+  int b = 0;
+  const hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx::body_kernel, oo_rx::WAVES_B * 64, 0);
+  return e == hipSuccess ? b : 0;
+}
+extern "C" int oo_rx_win_waves_per_block(void) { return oo_rx::WAVES_W; }
+extern "C" int oo_rx_body_waves_per_block(void) { return oo_rx::WAVES_B; }
+extern "C" int oo_rx_launch_win(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::win_kernel, dim3(grid), dim3(oo_rx::WAVES_W * 64), 0, stream, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int oo_rx_launch_body(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx::body_kernel, dim3(grid), dim3(oo_rx::WAVES_B * 64), 0, stream, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif  // OO_RX_SHORT

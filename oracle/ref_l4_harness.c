@@ -39,10 +39,26 @@
  *   S id af proto lport rport raddr flags hwports vlan
  *   A af sock laddr lport raddr rport proto     ci_netif_filter_insert
  *   P intf hexframe                             one frame ->
- *     "r handled kernel entry l4off ip_paylen n1 f1 n2 f2 n3 f3 hash fut"
+ *     "r handled kernel entry l4off ip_paylen n1 f1 n2 f2 n3 f3 hash fut
+ *        | eth ipcsum udp udpset tcp proto | name=delta ..."
  *     entry 0: no L4 handler ran, else 6 / 17; nK fK per lookup stage K the
  *     handler ran (-1 -1 if it did not); hash: stage-1 hash_out (TCP);
  *     fut: the pre-future's socket (-1 none, -2 not run).
+ *     Then what tells handle_rx_csum_bad's drop branches apart (several
+ *     share a counter or none, netif_event.c:1024-1127), observed on the
+ *     run: eth 4 / 6 / 0 -- its IPv4 or IPv6 branch ran (the IS_IP6 flag it
+ *     clears or sets, seen over two runs with the flag preset both ways), or
+ *     neither; ipcsum 1 if ci_ip_csum_partial ran (ci_ip_csum_correct,
+ *     :80-94); udp / tcp -1 if ci_udp_csum_correct (udp_rx.c:101-121) /
+ *     ef_tcp_checksum[_ip6]_is_correct (checksum.c:326-351) did not run, else
+ *     its verdict; udpset 1 if pkt->pf.udp.pay_len was written (:1105); proto
+ *     the protocol byte at the L3 offset ci_parse_rx_vlan left (-1: neither
+ *     branch).  Last, every stack counter the frame changed, by name, with
+ *     its delta: ni->state->stats_snapshot's ip / tcp / udp / tcp_ext groups
+ *     (ip_stats_ops.h:165-291) and ni->state->stats (stats_def.h,
+ *     CITP_STATS_NETIF_INC), over handle_rx_csum_bad and everything it ran
+ *     -- except the pre-future helpers this harness runs only to observe them
+ *     (their counter changes are undone).
  */
 #include "netif_event.c"                  /* -I src/lib/transport/ip */
 #include "udp_internal.h"
@@ -177,6 +193,95 @@ int __wrap_ci_netif_filter_for_each_match_ip6(ci_netif* n, const ci_addr_t* la, 
 }
 #endif
 
+/* ---- observed checksum checks */
+static int g_ipcsum, g_udpcsum, g_tcpcsum;
+
+extern unsigned __real_ci_ip_csum_partial(unsigned, const volatile void*, int);
+unsigned __wrap_ci_ip_csum_partial(unsigned sum, const volatile void* buf, int bytes)
+{
+  g_ipcsum = 1;
+  return __real_ci_ip_csum_partial(sum, buf, bytes);
+}
+
+extern int __real_ci_udp_csum_correct(ci_ip_pkt_fmt*, ci_udp_hdr*);
+int __wrap_ci_udp_csum_correct(ci_ip_pkt_fmt* pkt, ci_udp_hdr* udp)
+{
+  int rc = __real_ci_udp_csum_correct(pkt, udp);
+  g_udpcsum = rc != 0;
+  return rc;
+}
+
+extern int __real_ef_tcp_checksum_is_correct(const struct iphdr*, const struct tcphdr*,
+                                             const struct iovec*, int);
+int __wrap_ef_tcp_checksum_is_correct(const struct iphdr* ip, const struct tcphdr* tcp,
+                                      const struct iovec* iov, int iovlen)
+{
+  int rc = __real_ef_tcp_checksum_is_correct(ip, tcp, iov, iovlen);
+  g_tcpcsum = rc != 0;
+  return rc;
+}
+
+extern int __real_ef_tcp_checksum_ip6_is_correct(const struct ipv6hdr*, const struct tcphdr*,
+                                                 const struct iovec*, int);
+int __wrap_ef_tcp_checksum_ip6_is_correct(const struct ipv6hdr* ip6, const struct tcphdr* tcp,
+                                          const struct iovec* iov, int iovlen)
+{
+  int rc = __real_ef_tcp_checksum_ip6_is_correct(ip6, tcp, iov, iovlen);
+  g_tcpcsum = rc != 0;
+  return rc;
+}
+
+/* ---- stack counters around a frame */
+static ci_ip_stats g_ip0;
+static ci_netif_stats g_ni0;
+
+static void stats_save(ci_ip_stats* ip, ci_netif_stats* nst)
+{
+  memcpy(ip, &ni->state->stats_snapshot, sizeof(*ip));
+  memcpy(nst, &ni->state->stats, sizeof(*nst));
+}
+
+static void stats_restore(const ci_ip_stats* ip, const ci_netif_stats* nst)
+{
+  memcpy(&ni->state->stats_snapshot, ip, sizeof(*ip));
+  memcpy(&ni->state->stats, nst, sizeof(*nst));
+}
+
+static void stats_print_delta(const ci_ip_stats* a, const ci_netif_stats* na)
+{
+  const ci_ip_stats* b = &ni->state->stats_snapshot;
+  const ci_netif_stats* nb = &ni->state->stats;
+#define OO_STAT(desc, type, name, kind)                                        \
+  if( b->GRP.name != a->GRP.name )                                             \
+    printf(" " GRPS ".%s=%lld", #name, (long long) (b->GRP.name - a->GRP.name));
+#define GRP ip
+#define GRPS "ip"
+#include <ci/internal/ip_stats_count_def.h>
+#undef GRP
+#undef GRPS
+#define GRP tcp
+#define GRPS "tcp"
+#include <ci/internal/tcp_stats_count_def.h>
+#undef GRP
+#undef GRPS
+#define GRP udp
+#define GRPS "udp"
+#include <ci/internal/udp_stats_count_def.h>
+#undef GRP
+#undef GRPS
+#define GRP tcp_ext
+#define GRPS "tcp_ext"
+#include <ci/internal/tcp_ext_stats_count_def.h>
+#undef GRP
+#undef GRPS
+#undef OO_STAT
+#define OO_STAT(desc, type, name, kind)                                        \
+  if( nb->name != na->name )                                                   \
+    printf(" ni.%s=%lld", #name, (long long) (nb->name - na->name));
+#include <ci/internal/stats_def.h>
+#undef OO_STAT
+}
+
 /* ---- observed L4 entries */
 extern void __real_ci_udp_handle_rx(ci_netif*, ci_ip_pkt_fmt*, ci_udp_hdr*, int);
 void __wrap_ci_udp_handle_rx(ci_netif* n, ci_ip_pkt_fmt* pkt, ci_udp_hdr* udp, int ip_paylen)
@@ -186,9 +291,13 @@ void __wrap_ci_udp_handle_rx(ci_netif* n, ci_ip_pkt_fmt* pkt, ci_udp_hdr* udp, i
   R.ip_paylen = ip_paylen;
   if( oo_pkt_af(pkt) == AF_INET ) {
     struct ci_udp_rx_future fut;
+    static ci_ip_stats ip;
+    static ci_netif_stats nst;
+    stats_save(&ip, &nst);
     g_passthrough = 1;
     ci_udp_handle_rx_pre_future(n, pkt, udp, ip_paylen, CI_ETHERTYPE_IP, &fut);
     g_passthrough = 0;
+    stats_restore(&ip, &nst);
     R.fut = fut.socket ? sock_id(&fut.socket->s) : -1;
   }
   __real_ci_udp_handle_rx(n, pkt, udp, ip_paylen);
@@ -204,9 +313,13 @@ void __wrap_ci_tcp_handle_rx(ci_netif* n, struct ci_netif_poll_state* ps, ci_ip_
   R.ip_paylen = ip_paylen;
   if( oo_pkt_af(pkt) == AF_INET ) {
     struct ci_tcp_rx_future fut;
+    static ci_ip_stats ip;
+    static ci_netif_stats nst;
+    stats_save(&ip, &nst);
     g_passthrough = 1;
     ci_tcp_handle_rx_pre_future(n, pkt, tcp, ip_paylen, &fut);
     g_passthrough = 0;
+    stats_restore(&ip, &nst);
     R.fut = fut.socket ? sock_id(fut.socket) : -1;
   }
   __real_ci_tcp_handle_rx(n, ps, pkt, tcp, ip_paylen);
@@ -287,11 +400,9 @@ static void do_sock(int id, int af, int proto, unsigned lport, unsigned rport,
 }
 
 /* ---- one frame through handle_rx_csum_bad */
-static void do_frame(int intf, const char* hex)
+static ci_ip_pkt_fmt* frame_pkt(int intf, const char* hex, int len, int ip6_preset)
 {
   static ci_ip_pkt_fmt* pkt;
-  static struct ci_netif_poll_state ps;
-  int len = (int) strlen(hex) / 2, handled, i;
   if( pkt == NULL )
     pkt = aligned_alloc(4096, 64 * 1024);
   memset(pkt, 0, sizeof(*pkt));
@@ -300,19 +411,60 @@ static void do_frame(int intf, const char* hex)
   pkt->frag_next = OO_PP_NULL;
   pkt->refcount = 1 << 20;
   pkt->intf_i = (ci_int16) intf;
+  if( ip6_preset )
+    pkt->flags |= CI_PKT_FLAG_IS_IP6;
+  pkt->pf.udp.pay_len = 0xdeadbeefu;
+  hexbytes(hex, (unsigned char*) PKT_START(pkt), len);
+  return pkt;
+}
+
+static void do_frame(int intf, const char* hex)
+{
+  static struct ci_netif_poll_state ps;
+  ci_ip_pkt_fmt* pkt;
+  int len = (int) strlen(hex) / 2, handled, i, eth = 0, udpset, proto = -1, f1, f2;
+  int ipcsum, udpc, tcpc;
   if( len > 64 * 1024 - (int) CI_MEMBER_OFFSET(ci_ip_pkt_fmt, dma_start) - 64 ) {
     printf("toolong\n");
     return;
   }
-  hexbytes(hex, (unsigned char*) PKT_START(pkt), len);
+  /* Run 1 (IS_IP6 preset): the record, the counters, the checks. */
+  pkt = frame_pkt(intf, hex, len, 1);
   memset(&R, 0, sizeof(R));
   for( i = 0; i < 3; ++i )
     R.n[i] = R.first[i] = -1;
   R.fut = -2;
+  g_ipcsum = 0;
+  g_udpcsum = g_tcpcsum = -1;
+  stats_save(&g_ip0, &g_ni0);
   handled = handle_rx_csum_bad(ni, &ps, pkt, len);
-  printf("r %d %d %d %d %d %d %d %d %d %d %d %u %d\n", handled, R.kernel, R.entry, R.l4off,
+  f1 = (pkt->flags & CI_PKT_FLAG_IS_IP6) != 0;
+  udpset = pkt->pf.udp.pay_len != 0xdeadbeefu;
+  ipcsum = g_ipcsum;
+  udpc = g_udpcsum;
+  tcpc = g_tcpcsum;
+  printf("r %d %d %d %d %d %d %d %d %d %d %d %u %d", handled, R.kernel, R.entry, R.l4off,
          R.ip_paylen, R.n[0], R.first[0], R.n[1], R.first[1], R.n[2], R.first[2], R.hash,
          R.fut);
+  /* Run 2 (IS_IP6 clear), a dropped frame only (no handler runs): which
+   * address-family branch wrote the flag.  Its counters are undone. */
+  if( ! handled ) {
+    static ci_ip_stats ip;
+    static ci_netif_stats nst;
+    stats_save(&ip, &nst);
+    pkt = frame_pkt(intf, hex, len, 0);
+    (void) handle_rx_csum_bad(ni, &ps, pkt, len);
+    f2 = (pkt->flags & CI_PKT_FLAG_IS_IP6) != 0;
+    stats_restore(&ip, &nst);
+    eth = (f1 && f2) ? 6 : (! f1 && ! f2) ? 4 : 0;
+    if( eth && pkt->pkt_eth_payload_off != PKT_START_OFF_BAD ) {
+      const unsigned char* l3 = (const unsigned char*) PKT_START(pkt) + pkt->pkt_eth_payload_off;
+      proto = l3[eth == 4 ? 9 : 6];
+    }
+  }
+  printf(" | %d %d %d %d %d %d |", eth, ipcsum, udpc, udpset, tcpc, proto);
+  stats_print_delta(&g_ip0, &g_ni0);
+  printf("\n");
 }
 
 int main(void)

@@ -12,8 +12,14 @@ stores what the reference answered for every frame:
                    ip_paylen, n1, first1, n2, first2, n3, first3, hash (TCP
                    stage 1), fut (pre-future socket; -1 none, -2 not run)
                    -- columns as tests/l4_ref.py names them
+  <corpus>/obs     int64 (n, 6): what tells handle_rx_csum_bad's drop
+                   branches apart -- eth, ipcsum, udp, udpset, tcp, proto
+                   (tests/l4_ref.py OBS; oracle/ref_l4_harness.c)
+  <corpus>/stats   int64 (n, K): each stack counter's change over the frame
+                   (columns: stats_names)
   <corpus>/sha256  SHA-256 of the frames (the test regenerates them and
                    checks this first: the fixture holds no frame bytes)
+  stats_names      the K counter names ("ip.in_recvs", "ni.ip_options", ...)
 
 Run: python tests/golden/make_l4_golden.py   (after `make -C oracle`)."""
 from __future__ import annotations
@@ -44,16 +50,28 @@ def run(corpus: str):
     nset = len(lines) - len(frames)
     assert len(out) == len(lines), (len(out), len(lines), p.stderr[-500:])
     assert all(x in ("ok", "0") for x in out[:nset]), [x for x in out[:nset] if x not in ("ok", "0")]
-    rows = [list(map(int, x.split()[1:])) for x in out[nset:]]
     assert all(x.startswith("r ") for x in out[nset:])
-    return np.array(rows, dtype=np.int64), l4_ref.frames_sha(frames)
+    rows, obs, stats = [], [], []
+    for x in out[nset:]:
+        a, b, c = x.split("|")
+        rows.append(list(map(int, a.split()[1:])))
+        obs.append(list(map(int, b.split())))
+        stats.append({k: int(v) for k, v in (t.split("=") for t in c.split())})
+    return (np.array(rows, dtype=np.int64), np.array(obs, dtype=np.int64), stats,
+            l4_ref.frames_sha(frames))
 
 
 def main() -> None:
-    res = {}
+    res, runs = {}, {}
     for name in l4_ref.CORPORA:
-        out, sha = run(name)
+        runs[name] = run(name)
+    names = sorted({k for r in runs.values() for d in r[2] for k in d})
+    res["stats_names"] = np.array(names)
+    for name, (out, obs, stats, sha) in runs.items():
         res[f"{name}/out"] = out
+        res[f"{name}/obs"] = obs
+        res[f"{name}/stats"] = np.array([[d.get(k, 0) for k in names] for d in stats],
+                                        dtype=np.int64).reshape(len(stats), len(names))
         res[f"{name}/sha256"] = np.frombuffer(bytes.fromhex(sha), np.uint8)
         handled = out[:, 0].sum()
         print(f"{name}: {len(out)} frames, {handled} handled, "

@@ -17,7 +17,17 @@ What the reference's run pins, per frame:
   kernel    ci_netif_pkt_pass_to_kernel was called (NO_MATCH, IP4_FRAG,
             IP4_OPTS_BAD, TCP_SCATTERED);
   fut       the socket ci_udp_handle_rx_pre_future / ci_tcp_handle_rx_pre_
-            future resolve (udp_internal.h:41-103, tcp_rx.h:150-184; IPv4).
+            future resolve (udp_internal.h:41-103, tcp_rx.h:150-184; IPv4);
+  obs       which of handle_rx_csum_bad's drop branches a dropped frame took
+            (netif_event.c:1024-1127), from what the run shows: the
+            address-family branch that ran, which checksum functions ran and
+            their verdicts, whether pf.udp.pay_len was written, the protocol
+            byte (OBS; ref_drop_reasons);
+  stats     every stack counter the frame changed and by how much
+            (ip_stats_ops.h:165-291, stats_def.h via CITP_STATS_NETIF_INC):
+            the drop counters of handle_rx_csum_bad, handle_rx_pkt's
+            in_recvs / in_delivers / in_discards / ip_options, the handlers'
+            udp_in_dgrams / tcp_in_segs / no-match counters (expected_stats).
 """
 from __future__ import annotations
 
@@ -96,6 +106,112 @@ def world_script(socks, filters, hwports):
 
 def load(golden, name):
     return golden[f"{name}/out"], bytes(golden[f"{name}/sha256"]).hex()
+
+
+OBS = ("eth", "ipcsum", "udp", "udpset", "tcp", "proto")
+
+
+def load_stats(golden, name):
+    """(obs (n, 6), [{counter: delta}] per frame) of a corpus."""
+    names = [str(x) for x in golden["stats_names"]]
+    st = golden[f"{name}/stats"]
+    return golden[f"{name}/obs"], [{k: int(v) for k, v in zip(names, row) if v} for row in st]
+
+
+def ref_drop_reasons(o, st) -> set:
+    """The drop reasons handle_rx_csum_bad's observed run allows
+    (netif_event.c:1024-1127): its branches by the counter they bump
+    (in_hdr_errs :1031/:1048/:1055, in6_hdr_errs :1069, udp_in_errs :1116),
+    the address-family branch that ran (it writes CI_PKT_FLAG_IS_IP6 first,
+    :1043/:1063), whether ci_ip_csum_partial ran (:1053), the checksum
+    functions' verdicts (:1091, :1109), whether pf.udp.pay_len was written
+    (:1105) and the protocol byte.  TCP's two gates before its checksum
+    function (ip_paylen < 20, :1087; doff < 5 or hlen > ip_paylen inside
+    ci_tcp_csum_correct, :107-110) leave the same trace: that pair is
+    allowed either way."""
+    o = dict(zip(OBS, (int(x) for x in o)))
+    if st.get("ip.in_hdr_errs"):
+        if o["eth"] == 0:
+            return {_abi.R_SHORT_L2}
+        return {_abi.R_IP4_CSUM} if o["ipcsum"] else {_abi.R_IP4_LEN}
+    if st.get("ip.in6_hdr_errs"):
+        return {_abi.R_IP6_LEN}
+    if st.get("udp.udp_in_errs") or o["udp"] == 0:
+        return {_abi.R_UDP_CSUM}
+    if o["eth"] == 0:
+        return {_abi.R_NOT_IP}
+    if o["udpset"] and o["udp"] == -1:
+        return {_abi.R_UDP_SHORT}
+    if o["tcp"] == 0:
+        return {_abi.R_TCP_CSUM}
+    if o["proto"] == 6:
+        return {_abi.R_TCP_SHORT, _abi.R_TCP_CSUM}
+    if o["proto"] not in (6, 17):
+        return {_abi.R_PROTO_OTHER}
+    return set()
+
+
+def expected_stats(r) -> dict:
+    """The stack counters the reference's per-event path changes for a frame
+    whose record is r: handle_rx_csum_bad's drop counters, then for a handled
+    frame handle_rx_pkt (netif_event.c:282-373 / :384-404: in_recvs, the
+    option parse's ip_options or rx_discard_ip_options_bad + in_hdr_errs
+    :179-183, in_discards + the pass to the kernel for the slow path,
+    in_delivers) and the handler (udp_rx.c:263 udp_in_dgrams, :322-327
+    no-match to the kernel; tcp_rx.c:4692 tcp_in_segs, :4842-4857 no match
+    or scattered to the kernel).  The poll shim keeps the ones it replaces
+    (INTEGRATION.md §2); tests pin this against the reference's run."""
+    reason = int(r["reason"])
+    d = {}
+    if reason >= _abi.R_DROP_BASE:
+        if reason in (_abi.R_SHORT_L2, _abi.R_IP4_LEN, _abi.R_IP4_CSUM):
+            d["ip.in_hdr_errs"] = 1
+        elif reason == _abi.R_IP6_LEN:
+            d["ip.in6_hdr_errs"] = 1
+        elif reason == _abi.R_UDP_CSUM:
+            d["udp.udp_in_errs"] = 1
+        return d
+    is6 = bool(int(r["flags"]) & _abi.F_IP6)
+    d["ip.in6_recvs" if is6 else "ip.in_recvs"] = 1
+    if reason in (_abi.R_IP4_FRAG, _abi.R_IP4_OPTS_BAD):
+        d["ip.in_discards"] = 1
+        d["ni.no_match_pass_to_kernel_ip_other"] = 1
+        if reason == _abi.R_IP4_OPTS_BAD:
+            d["ip.in_hdr_errs"] = 1
+            d["ni.rx_discard_ip_options_bad"] = 1
+        return d
+    d["ip.in6_delivers" if is6 else "ip.in_delivers"] = 1
+    pre_l3 = 18 if int(r["flags"]) & _abi.F_VLAN else 14
+    if not is6 and int(r["l4_off"]) > pre_l3 + 20:
+        d["ni.ip_options"] = 1
+    if int(r["proto"]) == 17:
+        d["udp.udp_in_dgrams"] = 1
+        if reason == _abi.R_NO_MATCH:
+            d["ni.no_match_pass_to_kernel_udp"] = 1
+    else:
+        d["tcp.tcp_in_segs"] = 1
+        if reason in (_abi.R_NO_MATCH, _abi.R_TCP_SCATTERED):
+            d["ni.no_match_pass_to_kernel_tcp"] = 1
+    return d
+
+
+def stats_mismatches(recs, obs, stats, limit: int = 8) -> list[str]:
+    """Where the records' drop reasons or counter changes disagree with the
+    reference's run (empty: none)."""
+    bad = []
+    for i, (r, o, st) in enumerate(zip(recs, obs, stats)):
+        err = []
+        reason = int(r["reason"])
+        if reason >= _abi.R_DROP_BASE and reason not in ref_drop_reasons(o, st):
+            err.append(f"drop reason {reason} not in {sorted(ref_drop_reasons(o, st))}")
+        want = expected_stats(r)
+        if want != st:
+            err.append(f"stats {want} != reference {st}")
+        if err:
+            bad.append(f"[{i}] {', '.join(err)}: rec={r} obs={dict(zip(OBS, o.tolist()))}")
+            if len(bad) >= limit:
+                break
+    return bad
 
 
 KERNEL = (_abi.R_NO_MATCH, _abi.R_IP4_FRAG, _abi.R_IP4_OPTS_BAD, _abi.R_TCP_SCATTERED)

@@ -25,9 +25,11 @@ def cuda():
 
 
 @pytest.mark.parametrize("name", l4_ref.CORPORA)
-@pytest.mark.parametrize("kernel", (1, 2))
+@pytest.mark.parametrize("kernel", (0, 1, 2))
 def test_gpu_matches_reference_run(cuda, monkeypatch, name, kernel):
-    monkeypatch.setenv("OO_RX_KERNEL", str(kernel))  # both rx_kernel instances
+    # 0: the split transform (win_kernel + body_kernel), 1 / 2: the
+    # single-kernel instances
+    monkeypatch.setenv("OO_RX_KERNEL", str(kernel))
     out, sha = l4_ref.load(np.load(GOLDEN), name)
     socks, filters, hwports, frames = l4_ref.corpus(name)
     assert l4_ref.frames_sha(frames) == sha
@@ -40,4 +42,7 @@ def test_gpu_matches_reference_run(cuda, monkeypatch, name, kernel):
     recs, _ = run_dev(g, buf, desc)
     g.close()
     bad = l4_ref.mismatches(recs, out)
+    assert not bad, "\n".join(bad)
+    obs, stats = l4_ref.load_stats(np.load(GOLDEN), name)
+    bad = l4_ref.stats_mismatches(recs, obs, stats)
     assert not bad, "\n".join(bad)

@@ -112,3 +112,64 @@ def test_poll_stage_routing(cuda):
         g.filter_remove(*filters[stage - 1])
     assert seen == ["future", "full", "full"]
     g.close()
+
+
+# The per-record counters the shim keeps (src/shim/oo_rx_poll.c count_drop /
+# dispatch) -> the reference counter whose per-frame changes they replace.
+SHIM_DROP = {"in_hdr_errs": "ip.in_hdr_errs", "in6_hdr_errs": "ip.in6_hdr_errs",
+             "udp_in_errs": "udp.udp_in_errs"}
+SHIM_HANDLED = {"in_recvs": "ip.in_recvs", "in_delivers": "ip.in_delivers",
+                "in6_recvs": "ip.in6_recvs", "in6_delivers": "ip.in6_delivers",
+                "ip_options": "ni.ip_options"}
+SHIM_FUTURE = {"tcp_in_segs": "tcp.tcp_in_segs", "udp_in_dgrams": "udp.udp_in_dgrams"}
+
+
+@pytest.mark.parametrize("name", ("edge", "edge99", "c2", "c4", "c5"))
+def test_poll_counters_match_reference_run(cuda, name):
+    """The shim's per-record stack counters against the reference's own run
+    of the same frames (tests/golden/ref_l4_golden.npz: every counter
+    handle_rx_csum_bad, handle_rx_pkt and the handlers changed, per frame):
+    the drop counters over the dropped frames, handle_rx_pkt's over the
+    frames an L4 handler took (the slow-path ones go to ops->pkt_handler,
+    which is handle_rx_pkt and counts for itself), the handlers' in_segs /
+    in_dgrams over the frames whose future resolved (the post-future helpers
+    count them, tcp_rx.h:182, udp_internal.h:99; the full handlers count
+    the rest themselves).  rx_evs / rx_discard_* / rx_sw_csum_pass belong to
+    the poll loop around handle_rx_csum_bad (netif_event.c:1164-1191,
+    :1718), which the harness does not run: test_poll_dispatch_and_counters
+    checks them."""
+    import l4_ref
+    from test_oracle_l4_ref import GOLDEN
+    golden = np.load(GOLDEN)
+    out, sha = l4_ref.load(golden, name)
+    obs, stats = l4_ref.load_stats(golden, name)
+    socks, filters, hwports, frames = l4_ref.corpus(name)
+    assert l4_ref.frames_sha(frames) == sha
+    g = GpuRxStack(device=0, intf_hwport=hwports, host_stage_bytes=64 << 20,
+                   host_stage_pkts=65536)
+    for i, s in socks.items():
+        assert g.sock_set(i, s) == 0
+    for (i, af, la, lp, ra, rp, proto) in filters:
+        assert g.filter_insert_raw(i, af, la, lp, ra, rp, proto) == 0
+    pool, evs = events_for(frames, BUF, np.random.default_rng(5), discard_mix=False)
+    rec = Recorder()
+    p = poll.RxPoll(g, pool, BUF, 64, True, rec)
+    assert p.poll(evs) == len(evs)
+    st = p.stats.as_dict()
+    c = {k: out[:, i] for i, k in enumerate(l4_ref.COLS)}
+    dropped = c["handled"] == 0
+    took = (c["handled"] == 1) & (c["entry"] != 0)
+    fut = took & (c["fut"] >= 0)
+    want = {}
+    for k, ref in SHIM_DROP.items():
+        want[k] = sum(stats[i].get(ref, 0) for i in np.flatnonzero(dropped))
+    for k, ref in SHIM_HANDLED.items():
+        want[k] = sum(stats[i].get(ref, 0) for i in np.flatnonzero(took))
+    for k, ref in SHIM_FUTURE.items():
+        want[k] = sum(stats[i].get(ref, 0) for i in np.flatnonzero(fut))
+    got = {k: st[k] for k in want}
+    assert got == want
+    assert st["n_future"] == int(fut.sum())
+    assert st["n_pkt_handler"] == int(((c["handled"] == 1) & (c["entry"] == 0)).sum())
+    p.close()
+    g.close()

@@ -81,13 +81,14 @@ def test_store_counts(asm):
     # store_records: two 16-B stores per tile (NST)
     assert len(re.findall(r"global_store_dwordx4", rx)) == 2
     assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
-    assert len(re.findall(r"global_store_dword .* sc1$", rx, re.M)) == 1  # claim_next
-    assert len(re.findall(r"global_store_dword\b", rx)) == 1
+    # zero_claim_set: the next launch's claim set, three `sc1` stores
+    assert len(re.findall(r"global_store_dword .* sc1$", rx, re.M)) == 3
+    assert len(re.findall(r"global_store_dword\b", rx)) == 3
     tx = _body(text, "_ZN5oo_rx9tx_kernelENS_7KParamsE")
     assert len(re.findall(r"global_store_short\b", tx)) == 2
     assert len(re.findall(r"global_store_dwordx4", tx)) == 4
     assert not re.findall(r"global_store_(byte|dwordx2)", tx)
-    assert len(re.findall(r"global_store_dword\b", tx)) == 1
+    assert len(re.findall(r"global_store_dword\b", tx)) == 3
     for body in (rx, tx):  # flat stores would count in lgkmcnt as well
         assert not re.findall(r"flat_store|flat_load|flat_atomic", body)
 
@@ -101,5 +102,5 @@ def test_short_kernel_same_invariants(asm_short):
     assert "scratch_" not in rx
     assert len(re.findall(r"global_store_dwordx4", rx)) == 2
     assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
-    assert len(re.findall(r"global_store_dword\b", rx)) == 1  # claim_next
+    assert len(re.findall(r"global_store_dword\b", rx)) == 3  # zero_claim_set
     assert not re.findall(r"flat_store|flat_load|flat_atomic", rx)

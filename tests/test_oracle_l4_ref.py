@@ -16,6 +16,7 @@ import pytest
 
 import l4_ref
 from frames import pack
+from onload_amd import _abi
 from oracle_lib import OracleStack
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -45,6 +46,40 @@ def test_oracle_matches_reference_run(name):
     assert not bad, "\n".join(bad)
 
 
+@pytest.mark.parametrize("name", l4_ref.CORPORA)
+def test_oracle_drop_reasons_and_counters_match_reference_run(name):
+    """Every dropped frame's reason is the branch handle_rx_csum_bad took
+    (TCP's two pre-checksum gates: either of their two reasons), and every
+    frame changes exactly the stack counters the reference's run changed."""
+    golden = np.load(GOLDEN)
+    obs, stats = l4_ref.load_stats(golden, name)
+    recs, _ = oracle_records(name)
+    bad = l4_ref.stats_mismatches(recs, obs, stats)
+    assert not bad, "\n".join(bad)
+
+
+def test_fixture_covers_every_drop_branch():
+    """The corpora reach all ten drop branches, told apart by the reference's
+    own run, and every counter the rules name."""
+    golden = np.load(GOLDEN)
+    seen, names = set(), set()
+    for n in l4_ref.CORPORA:
+        out, _ = l4_ref.load(golden, n)
+        obs, stats = l4_ref.load_stats(golden, n)
+        for row, o, st in zip(out, obs, stats):
+            names |= set(st)
+            if row[0] == 0:
+                rs = l4_ref.ref_drop_reasons(o, st)
+                assert rs, (o, st)
+                seen |= rs
+    assert seen == set(range(_abi.R_DROP_BASE, _abi.R_UDP_CSUM + 1))
+    assert {"ip.in_hdr_errs", "ip.in6_hdr_errs", "udp.udp_in_errs", "ip.in_recvs",
+            "ip.in_delivers", "ip.in6_recvs", "ip.in6_delivers", "ip.in_discards",
+            "ni.ip_options", "ni.rx_discard_ip_options_bad", "udp.udp_in_dgrams",
+            "tcp.tcp_in_segs", "ni.no_match_pass_to_kernel_udp",
+            "ni.no_match_pass_to_kernel_tcp", "ni.no_match_pass_to_kernel_ip_other"} <= names
+
+
 def test_fixture_covers_the_rules():
     """The corpora reach every decision the fixture pins: all three TCP
     stages, both UDP stages with multi-match, the UDP future given up by a
@@ -72,6 +107,13 @@ def test_fixture_rederived_live(name):
         [f"P {intf} {f.hex()}" for f, intf in frames]
     p = subprocess.run([HARNESS], input="\n".join(lines) + "\n", capture_output=True, text=True,
                        check=True)
-    rows = np.array([list(map(int, x.split()[1:])) for x in p.stdout.splitlines()
-                     if x.startswith("r ")], dtype=np.int64)
-    np.testing.assert_array_equal(rows, l4_ref.load(np.load(GOLDEN), name)[0])
+    lines = [x for x in p.stdout.splitlines() if x.startswith("r ")]
+    golden = np.load(GOLDEN)
+    rows = np.array([list(map(int, x.split("|")[0].split()[1:])) for x in lines], dtype=np.int64)
+    obs = np.array([list(map(int, x.split("|")[1].split())) for x in lines], dtype=np.int64)
+    stats = [{k: int(v) for k, v in (t.split("=") for t in x.split("|")[2].split())}
+             for x in lines]
+    np.testing.assert_array_equal(rows, l4_ref.load(golden, name)[0])
+    gobs, gstats = l4_ref.load_stats(golden, name)
+    np.testing.assert_array_equal(obs, gobs)
+    assert stats == gstats
