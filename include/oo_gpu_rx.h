@@ -227,6 +227,11 @@ int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* ctx, int32_t sock_id,
                        const oo_gpu_rx_sock* sock);
 /* Apply pending table/socket changes to the device on `stream` now. */
 int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* ctx, void* stream);
+/* The number of table and socket changes made on the context so far
+ * (insert, remove, sock_set, import): a caller that has batches in flight
+ * compares it across its own callbacks to learn whether a batch submitted
+ * before them was transformed on tables that have since changed. */
+uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* ctx);
 /* Streams.  The context remembers the streams it launched on (nothing is
  * recorded per batch): a table change enqueues an event on each of them at
  * that moment and waits for it, so every stream used with the context must

@@ -149,6 +149,10 @@ typedef struct oo_rx_poll_stats {
   uint64_t n_release;               /* release calls                             */
   uint64_t n_other;                 /* other_ev calls                            */
   uint64_t n_batches;               /* oo_gpu_rx_batch calls                     */
+  uint64_t n_resubmit;              /* chunks transformed again: a callback of the
+                                       chunk before changed the tables           */
+  uint64_t n_handback;              /* events of chunks left to the caller's
+                                       per-event path (OO_RX_POLL_CROSSOVER)     */
 } oo_rx_poll_stats;
 
 /* The callback table: the integration maps these onto the stack's functions
@@ -178,13 +182,31 @@ typedef struct oo_rx_poll_cfg {
                                north-star case); 0: only discard events in the
                                checksum class do (:1155-1162), plain RX events
                                go to other_ev                                  */
-  uint32_t    flags;        /* OO_RX_POLL_ZERO_COPY, or 0                      */
+  uint32_t    flags;        /* OO_RX_POLL_ZERO_COPY | OO_RX_POLL_CROSSOVER      */
+  /* The cost model OO_RX_POLL_CROSSOVER uses (0: the default of each, the
+   * values tools/poll_bench measured).  Per chunk of m frames
+   * and B frame bytes the device batch costs
+   *   gpu_fixed_ns + m gpu_pkt_ps + B gpu_byte_ps
+   * and the caller's own per-event path (handle_rx_csum_bad one event at a
+   * time) m cpu_pkt_ps + B cpu_byte_ps. */
+  uint32_t    cpu_pkt_ps;   /* the per-event CPU path: ps per frame           */
+  uint32_t    cpu_byte_ps;  /*   and per frame byte                           */
+  uint32_t    gpu_fixed_ns; /* the device batch: fixed ns per chunk           */
+  uint32_t    gpu_pkt_ps;   /*   ps per frame                                 */
+  uint32_t    gpu_byte_ps;  /*   ps per frame byte (gather: the host copy too) */
 } oo_rx_poll_cfg;
 
 /* cfg.flags: register pkt_bufs with the device and read frames in place
  * (falls back to gathering if the pool cannot be registered; see
  * oo_rx_poll_zero_copy). */
 #define OO_RX_POLL_ZERO_COPY 0x1u
+/* cfg.flags: a chunk whose device batch would cost more than the caller's
+ * own per-event path (the cost model above) is not transformed: all its
+ * events go to ops->other_ev unchanged and uncounted, exactly as if the
+ * shim were not there, so the caller's loop runs them one at a time
+ * (netif_event.c:1709-1742 / :1131-1191).  The branch is then never slower
+ * than the loop it replaces, by the model. */
+#define OO_RX_POLL_CROSSOVER 0x2u
 
 typedef struct oo_rx_poll oo_rx_poll;
 

@@ -163,16 +163,25 @@ static void gpu_add_stats(ci_netif* ni, const oo_rx_poll_stats* s)
 }
 
 /* Per-stack state: the device context, the shim and the callback context it
- * was opened with (ops.arg), refreshed for each poll. */
+ * was opened with (ops.arg), refreshed for each batch, and the RX events
+ * queued over one ci_netif_poll_evq pass (ci_netif_rx_gpu_queue): the
+ * shim's view of each and the original, for the existing loop. */
 struct ci_netif_gpu_rx {
   oo_gpu_rx_ctx* gpu;
   oo_rx_poll* poll;
   struct gpu_poll_ctx c;
+  int cap, n;                      /* queued events, capacity               */
+  oo_rx_poll_ev* q;
+  ef_event* orig;
+  uint8_t* handback;
 };
 
 /* At stack creation, next to ci_netif_filter_init (netif_init.c:105-108).
  * umem: the AF_XDP UMEM the RX ring's addresses index (chunk 2048,
- * tcp_helper_resource.c:2205-2208; efxdp_vi.c:337-348). */
+ * tcp_helper_resource.c:2205-2208; efxdp_vi.c:337-348).  The shim reads
+ * frames in place (the UMEM registered with the device) and leaves a pass
+ * whose batch would cost more than the per-event loop to that loop
+ * (OO_RX_POLL_CROSSOVER). */
 int ci_netif_rx_gpu_open(ci_netif* ni, struct ci_netif_gpu_rx* g, int device,
                          const void* umem, uint64_t umem_bytes)
 {
@@ -181,6 +190,14 @@ int ci_netif_rx_gpu_open(ci_netif* ni, struct ci_netif_gpu_rx* g, int device,
   oo_rx_poll_ops ops = { gpu_post_future, gpu_full_handler, gpu_pkt_handler,
                          gpu_release, gpu_other_ev, &g->c };
   int i, rc;
+  memset(g, 0, sizeof(*g));
+  /* A pass polls 16 events at a time until evs_per_poll (:1697, :1892). */
+  g->cap = NI_OPTS(ni).evs_per_poll + 16;
+  g->q = calloc(g->cap, sizeof(*g->q));
+  g->orig = calloc(g->cap, sizeof(*g->orig));
+  g->handback = calloc(g->cap, 1);
+  if( g->q == NULL || g->orig == NULL || g->handback == NULL )
+    return -ENOMEM;
   memset(&cfg, 0, sizeof(cfg));
   cfg.device = device;
   cfg.max_socks = ni->state->n_ep_bufs;
@@ -189,88 +206,124 @@ int ci_netif_rx_gpu_open(ci_netif* ni, struct ci_netif_gpu_rx* g, int device,
   cfg.n_intf = oo_stack_intf_max(ni);
   for( i = 0; i < cfg.n_intf; ++i )
     cfg.intf_hwport[i] = ni->state->intf_i_to_hwport[i];
-  cfg.host_stage_bytes = (uint64_t) NI_OPTS(ni).evs_per_poll * 2048;
-  cfg.host_stage_pkts = NI_OPTS(ni).evs_per_poll;
+  cfg.host_stage_bytes = (uint64_t) g->cap * 2048;
+  cfg.host_stage_pkts = g->cap;
   if( (rc = oo_gpu_rx_open(&g->gpu, &cfg)) < 0 )
     return rc;
   memset(&pcfg, 0, sizeof(pcfg));
   pcfg.pkt_bufs = umem;
   pcfg.pkt_bufs_bytes = umem_bytes;
   pcfg.buf_size = 2048;
-  pcfg.evs_per_poll = NI_OPTS(ni).evs_per_poll;
+  pcfg.evs_per_poll = g->cap;
   pcfg.sw_verify = 1;              /* AF_XDP: no NIC checksum verdict */
+  pcfg.flags = OO_RX_POLL_ZERO_COPY | OO_RX_POLL_CROSSOVER;
   g->c.ni = ni;
   if( (rc = oo_rx_poll_open(&g->poll, g->gpu, &pcfg, &ops)) < 0 )
     oo_gpu_rx_close(g->gpu);
   return rc;
 }
 
-/* The batched RX branch, in place of the per-event RX cases of
- * ci_netif_poll_evq (netif_event.c:1715-1742, :1843): the RX / RX_DISCARD
- * events of one ef_eventq_poll (:1697, at most 16 events; EF_EVS_PER_POLL
- * bounds a poll, opts_netif_def.h:976-984) of interface intf_i go to the
- * device in one batch.  Other events, the events the shim hands back
- * (other_ev) and -- if the device fails -- every RX event it did not get to,
- * are copied to leftover[] in their original order for the existing loop.
- * Returns how many. */
+/* The shim's view of an RX / RX_DISCARD event (netif_event.c:1717-1736,
+ * :1843): 1, or 0 for another event type. */
+static int gpu_ev(ci_netif* ni, ef_vi* evq, int intf_i, const ef_event* ev,
+                  oo_rx_poll_ev* e)
+{
+  oo_pkt_p pp;
+  ci_ip_pkt_fmt* pkt;
+  memset(e, 0, sizeof(*e));
+  if( EF_EVENT_TYPE(*ev) == EF_EVENT_TYPE_RX ) {
+    OO_PP_INIT(ni, pp, EF_EVENT_RX_RQ_ID(*ev));
+    pkt = PKT_CHK(ni, pp);
+    if( evq->nic_type.arch == EF_VI_ARCH_AF_XDP )   /* :1724-1727 */
+      pkt->pkt_start_off = ev->rx.ofs - CI_MEMBER_OFFSET(ci_ip_pkt_fmt, dma_start);
+    e->rq_id = EF_EVENT_RX_RQ_ID(*ev);
+    e->len = EF_EVENT_RX_BYTES(*ev) - evq->rx_prefix_len;
+    e->flags = ev->rx.flags;
+  }
+  else if( EF_EVENT_TYPE(*ev) == EF_EVENT_TYPE_RX_DISCARD ) {
+    OO_PP_INIT(ni, pp, EF_EVENT_RX_DISCARD_RQ_ID(*ev));
+    pkt = PKT_CHK(ni, pp);
+    e->rq_id = EF_EVENT_RX_DISCARD_RQ_ID(*ev);
+    e->len = EF_EVENT_RX_DISCARD_BYTES(*ev) - evq->rx_prefix_len;
+    e->flags = ev->rx_discard.flags;
+    e->discard = gpu_discard_flags(EF_EVENT_RX_DISCARD_TYPE(*ev));
+  }
+  else {
+    return 0;
+  }
+  e->ofs = (uint16_t)(pkt->pkt_start_off + CI_MEMBER_OFFSET(ci_ip_pkt_fmt, dma_start));
+  e->intf_i = (int16_t) intf_i;
+  pkt->pay_len = e->len;
+  return 1;
+}
+
+/* Inside ci_netif_poll_evq's do-loop, after each ef_eventq_poll (:1697): its
+ * RX and RX_DISCARD events join the pass's queue; every other event -- and
+ * any RX event the full queue cannot take -- is copied to other[] in order,
+ * for the loop's existing switch now.  Returns how many. */
+int ci_netif_rx_gpu_queue(ci_netif* ni, struct ci_netif_gpu_rx* g, ef_vi* evq,
+                          int intf_i, const ef_event* ev, int n_evs, ef_event* other)
+{
+  int i, n_other = 0;
+  for( i = 0; i < n_evs; ++i ) {
+    if( g->n < g->cap && gpu_ev(ni, evq, intf_i, &ev[i], &g->q[g->n]) ) {
+      g->orig[g->n] = ev[i];
+      ++g->n;
+    }
+    else {
+      other[n_other++] = ev[i];
+    }
+  }
+  return n_other;
+}
+
+/* Once per pass, after the do-loop (before :1915): the queued events as one
+ * batch.  Events the shim hands back (other_ev: not whole-buffer, outside
+ * the pool, or a pass the crossover leaves to the loop) and -- if the
+ * device fails -- every event it did not get to are copied to leftover[]
+ * (capacity g->cap) in their original order, for the existing per-event
+ * code.  Returns how many. */
+int ci_netif_rx_gpu_flush(ci_netif* ni, struct ci_netif_poll_state* ps,
+                          struct ci_netif_gpu_rx* g, ef_event* leftover)
+{
+  oo_rx_poll_stats st;
+  int i, handled, n_left = 0;
+  if( g->n == 0 )
+    return 0;
+  memset(&st, 0, sizeof(st));
+  memset(g->handback, 0, (size_t) g->n);
+  g->c.ps = ps;
+  g->c.evs = g->q;
+  g->c.handback = g->handback;
+  /* n, or fewer if the device failed part-way: events from `handled` on ran
+   * no callback and added no counter (oo_rx_poll.h) -- the CPU loop takes
+   * them, so nothing is released or delivered twice. */
+  handled = oo_rx_poll_evs(g->poll, g->q, (uint32_t) g->n, &st);
+  if( handled < 0 )
+    handled = 0;
+  gpu_add_stats(ni, &st);
+  for( i = 0; i < g->n; ++i )
+    if( i >= handled || g->handback[i] )
+      leftover[n_left++] = g->orig[i];
+  g->n = 0;
+  return n_left;
+}
+
+/* The one-call form for a loop left as it is: the events of one
+ * ef_eventq_poll (any number of them: the queue is flushed whenever it
+ * fills, nothing is dropped) in one batch.  other[] and leftover[] as above;
+ * returns how many events went to leftover[] (the non-RX ones first, then
+ * those the batch handed back). */
 int ci_netif_rx_batch_gpu(ci_netif* ni, struct ci_netif_poll_state* ps,
                           struct ci_netif_gpu_rx* g, ef_vi* evq, int intf_i,
                           const ef_event* ev, int n_evs, ef_event* leftover)
 {
-  enum { MAX_EVS = 64 };
-  oo_rx_poll_ev e[MAX_EVS];
-  int16_t shim_of[MAX_EVS];        /* original event -> shim index, or -1 */
-  uint8_t handback[MAX_EVS];
-  oo_rx_poll_stats st;
-  int i, n = 0, handled, n_left = 0;
-  if( n_evs > MAX_EVS )
-    n_evs = MAX_EVS;               /* the caller polls at most 16 at a time */
-  memset(&st, 0, sizeof(st));
-  memset(e, 0, sizeof(e));
-  memset(handback, 0, sizeof(handback));
-  g->c.ps = ps;
-  g->c.evs = e;
-  g->c.handback = handback;
-  for( i = 0; i < n_evs; ++i ) {
-    oo_pkt_p pp;
-    ci_ip_pkt_fmt* pkt;
-    shim_of[i] = -1;
-    if( EF_EVENT_TYPE(ev[i]) == EF_EVENT_TYPE_RX ) {
-      OO_PP_INIT(ni, pp, EF_EVENT_RX_RQ_ID(ev[i]));
-      pkt = PKT_CHK(ni, pp);
-      if( evq->nic_type.arch == EF_VI_ARCH_AF_XDP )   /* :1724-1727 */
-        pkt->pkt_start_off = ev[i].rx.ofs - CI_MEMBER_OFFSET(ci_ip_pkt_fmt, dma_start);
-      e[n].rq_id = EF_EVENT_RX_RQ_ID(ev[i]);
-      e[n].len = EF_EVENT_RX_BYTES(ev[i]) - evq->rx_prefix_len;
-      e[n].flags = ev[i].rx.flags;
-      e[n].discard = 0;
-    }
-    else if( EF_EVENT_TYPE(ev[i]) == EF_EVENT_TYPE_RX_DISCARD ) {
-      OO_PP_INIT(ni, pp, EF_EVENT_RX_DISCARD_RQ_ID(ev[i]));
-      pkt = PKT_CHK(ni, pp);
-      e[n].rq_id = EF_EVENT_RX_DISCARD_RQ_ID(ev[i]);
-      e[n].len = EF_EVENT_RX_DISCARD_BYTES(ev[i]) - evq->rx_prefix_len;
-      e[n].flags = ev[i].rx_discard.flags;
-      e[n].discard = gpu_discard_flags(EF_EVENT_RX_DISCARD_TYPE(ev[i]));
-    }
-    else {
-      continue;
-    }
-    e[n].ofs = (uint16_t)(pkt->pkt_start_off + CI_MEMBER_OFFSET(ci_ip_pkt_fmt, dma_start));
-    e[n].intf_i = (int16_t) intf_i;
-    e[n].rsvd = 0;
-    pkt->pay_len = e[n].len;
-    shim_of[i] = (int16_t) n++;
+  int done = 0, n_left = 0;
+  while( done < n_evs ) {
+    const int k = n_evs - done < g->cap - g->n ? n_evs - done : g->cap - g->n;
+    n_left += ci_netif_rx_gpu_queue(ni, g, evq, intf_i, ev + done, k, leftover + n_left);
+    done += k;
+    n_left += ci_netif_rx_gpu_flush(ni, ps, g, leftover + n_left);
   }
-  /* n, or fewer if the device failed part-way: events from `handled` on ran
-   * no callback and added no counter (oo_rx_poll.h) -- the CPU loop takes
-   * them, so nothing is released or delivered twice. */
-  handled = oo_rx_poll_evs(g->poll, e, (uint32_t) n, &st);
-  if( handled < 0 )
-    handled = 0;
-  gpu_add_stats(ni, &st);
-  for( i = 0; i < n_evs; ++i )
-    if( shim_of[i] < 0 || shim_of[i] >= handled || handback[shim_of[i]] )
-      leftover[n_left++] = ev[i];
   return n_left;
 }

@@ -194,6 +194,7 @@ struct oo_gpu_rx_ctx {
   std::vector<uint32_t> touched;                      // the last mirror op's probe walk
   uint32_t gen = 1;       // flush generation (sockgen marks)
   uint32_t tables_gen = 0;  // flushes done; streams wait for it via tables_ev
+  uint64_t changes = 0;     // table / socket changes made (oo_gpu_rx_table_gen)
   hipEvent_t tables_ev = nullptr;
   hipStream_t tables_stream = nullptr;
   OpStage stage[2];
@@ -868,6 +869,7 @@ int oo_gpu_rx_table_insert(oo_gpu_rx_ctx* c, int af, const void* laddr, uint16_t
   // The device replays the insert, -ENOBUFS included (its raised route
   // counts are part of the table state).
   push_op(c, tuple_op(oo_rx::OP_INSERT, af, laddr, lport, raddr, rport, proto, id));
+  ++c->changes;
   return rc;
 }
 
@@ -882,6 +884,7 @@ int oo_gpu_rx_table_remove(oo_gpu_rx_ctx* c, int af, const void* laddr, uint16_t
   else
     return -EINVAL;
   push_op(c, tuple_op(oo_rx::OP_REMOVE, af, laddr, lport, raddr, rport, proto, id));
+  ++c->changes;
   return 0;
 }
 
@@ -923,8 +926,11 @@ int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* c, int32_t id, const oo_gpu_rx_sock* s) {
   op.sock = id;
   op.u.s = *s;
   push_op(c, op);
+  ++c->changes;
   return 0;
 }
+
+uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* c) { return c == nullptr ? 0 : c->changes; }
 
 int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   if (c == nullptr) return -EINVAL;
@@ -949,6 +955,9 @@ int oo_gpu_rx_stream_done(oo_gpu_rx_ctx* c, void* stream) {
     if (hipEventRecord(t.ev, s) != hipSuccess) return -EIO;
     t.gone = true;  // ev now covers all of s's work; s is never touched again
   }
+  // The last table change ran on s: a stream created later may get the same
+  // handle, and must still wait for tables_ev.
+  if (c->tables_stream == s) c->tables_stream = nullptr;
   return 0;
 }
 
@@ -1044,6 +1053,7 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, vo
   c->tables_stream = s;
   t->tables_seen = c->tables_gen;
   c->failed = false;  // the whole table state was replaced on both sides
+  ++c->changes;
   return 0;
 }
 

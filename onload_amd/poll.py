@@ -38,7 +38,8 @@ STAT_NAMES = ("rx_evs", "rx_sw_csum_pass", "rx_discard_csum_bad", "rx_discard_le
               "rx_discard_crc_bad", "rx_discard_other", "ip_options", "in_recvs", "in_hdr_errs",
               "in_delivers", "in6_recvs", "in6_hdr_errs", "in6_delivers", "tcp_in_segs",
               "udp_in_dgrams", "udp_in_errs", "n_future", "n_future_declined", "n_full",
-              "n_pkt_handler", "n_release", "n_other", "n_batches")
+              "n_pkt_handler", "n_release", "n_other", "n_batches", "n_resubmit",
+              "n_handback")
 
 
 class Stats(ctypes.Structure):
@@ -73,10 +74,14 @@ class Ops(ctypes.Structure):
 class PollCfg(ctypes.Structure):
     _fields_ = [("pkt_bufs", ctypes.c_void_p), ("pkt_bufs_bytes", ctypes.c_uint64),
                 ("buf_size", ctypes.c_uint32), ("evs_per_poll", ctypes.c_uint32),
-                ("sw_verify", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("sw_verify", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("cpu_pkt_ps", ctypes.c_uint32), ("cpu_byte_ps", ctypes.c_uint32),
+                ("gpu_fixed_ns", ctypes.c_uint32), ("gpu_pkt_ps", ctypes.c_uint32),
+                ("gpu_byte_ps", ctypes.c_uint32)]
 
 
 ZERO_COPY = 0x1  # OO_RX_POLL_ZERO_COPY
+CROSSOVER = 0x2  # OO_RX_POLL_CROSSOVER
 
 
 POLL_SYMBOLS = {
@@ -122,7 +127,8 @@ class RxPoll:
     alive by this object)."""
 
     def __init__(self, stack, pool: np.ndarray, buf_size: int, evs_per_poll: int,
-                 sw_verify: bool, handlers, zero_copy: bool = False):
+                 sw_verify: bool, handlers, zero_copy: bool = False,
+                 crossover: dict | None = None):
         self._lib = load_poll()
         self.pool = pool
         self.h = handlers
@@ -137,7 +143,9 @@ class RxPoll:
                            np.frombuffer(ctypes.string_at(e, 16), EV_DTYPE)[0])),
                        None)
         cfg = PollCfg(pool.ctypes.data, pool.nbytes, buf_size, evs_per_poll, int(sw_verify),
-                      ZERO_COPY if zero_copy else 0)
+                      (ZERO_COPY if zero_copy else 0) | (CROSSOVER if crossover is not None else 0))
+        for k, v in (crossover or {}).items():  # cost-model fields (0: defaults)
+            setattr(cfg, k, int(v))
         p = ctypes.c_void_p()
         rc = self._lib.oo_rx_poll_open(ctypes.byref(p), stack._ctx, ctypes.byref(cfg),
                                        ctypes.byref(self._cb))

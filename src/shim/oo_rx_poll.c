@@ -134,7 +134,7 @@ int oo_rx_poll_open(oo_rx_poll** out, oo_gpu_rx_ctx* gpu, const oo_rx_poll_cfg* 
   if( n == 0 || n > OO_RX_POLL_MAX_EVS || cfg->buf_size == 0 ||
       (cfg->buf_size & (cfg->buf_size - 1)) != 0 || cfg->buf_size > 65536 ||
       (cfg->pkt_bufs == NULL && cfg->pkt_bufs_bytes != 0) ||
-      (cfg->flags & ~(uint32_t)OO_RX_POLL_ZERO_COPY) != 0 )
+      (cfg->flags & ~(uint32_t)(OO_RX_POLL_ZERO_COPY | OO_RX_POLL_CROSSOVER)) != 0 )
     return -EINVAL;
   if( ops->post_future == NULL || ops->full_handler == NULL ||
       ops->pkt_handler == NULL || ops->release == NULL || ops->other_ev == NULL )
@@ -333,6 +333,24 @@ static void dispatch(oo_rx_poll* p, uint32_t id, const uint8_t* frame,
     ++st->in_delivers;                                     /* :327 / :332 */
 }
 
+/* The crossover's cost model (oo_rx_poll.h): whether the device batch of m
+ * frames and `bytes` frame bytes costs less than the caller's per-event
+ * path.  The defaults are tools/poll_bench's fits on MI355X boxes
+ * (DESIGN.md §5e): the per-event path 20.3 ns per frame + 0.146 ns per byte
+ * on one host core; a device batch ~30 us fixed (launches, completion,
+ * PCIe latency) + 15.2 ns per frame, + 0.029 ns per byte read in place
+ * (zero copy) or 0.081 ns per byte gathered (the host memcpy). */
+static int gpu_pays(const oo_rx_poll* p, uint64_t m, uint64_t bytes)
+{
+  const oo_rx_poll_cfg* c = &p->cfg;
+  const uint64_t cpu_pkt = c->cpu_pkt_ps ? c->cpu_pkt_ps : 20300;
+  const uint64_t cpu_byte = c->cpu_byte_ps ? c->cpu_byte_ps : 146;
+  const uint64_t fixed = (uint64_t)(c->gpu_fixed_ns ? c->gpu_fixed_ns : 30000) * 1000u;
+  const uint64_t gpu_pkt = c->gpu_pkt_ps ? c->gpu_pkt_ps : 15200;
+  const uint64_t gpu_byte = c->gpu_byte_ps ? c->gpu_byte_ps : (p->zero_copy ? 29 : 81);
+  return fixed + m * gpu_pkt + bytes * gpu_byte < m * cpu_pkt + bytes * cpu_byte;
+}
+
 /* Steps 1-2 for the chunk evs[0..n): classify, describe, submit.  0 or
  * -errno (the chunk is then not in flight and nothing was counted). */
 static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs, uint32_t n,
@@ -346,8 +364,26 @@ static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs
   c->busy = 0;
   c->st = *base;
   for( i = 0; i < n; ++i ) {
+    c->what[i] = (uint8_t)classify(p, &evs[i], &c->st);
+    if( c->what[i] == W_TRANSFORM ) {
+      total += evs[i].len;
+      ++m;
+    }
+  }
+  c->m = m;
+  if( m == 0 )
+    return 0;
+  if( (p->cfg.flags & OO_RX_POLL_CROSSOVER) && !gpu_pays(p, m, total) ) {
+    /* Cheaper one event at a time: the whole chunk goes back, uncounted. */
+    for( i = 0; i < n; ++i )
+      c->what[i] = W_OTHER;
+    c->st = *base;
+    c->st.n_handback += n;
+    c->m = 0;
+    return 0;
+  }
+  for( i = 0, m = 0; i < n; ++i ) {
     const oo_rx_poll_ev* e = &evs[i];
-    c->what[i] = (uint8_t)classify(p, e, &c->st);
     if( c->what[i] == W_TRANSFORM ) {
       oo_gpu_pkt_desc* d = &c->desc[m];
       if( p->zero_copy ) {
@@ -365,13 +401,9 @@ static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs
       d->len = e->len;
       d->intf_i = e->intf_i;
       d->rsvd = 0;
-      total += e->len;
       c->ev_of[m++] = i;
     }
   }
-  c->m = m;
-  if( m == 0 )
-    return 0;
   if( p->zero_copy ) {
     /* The frames sit in their 2048-B packet buffers, so the buffer bytes per
      * packet say nothing of their length: the poll's mean length picks the
@@ -456,6 +488,7 @@ int oo_rx_poll_evs(oo_rx_poll* p, const oo_rx_poll_ev* evs, uint32_t n,
     struct chunk* c = &p->ch[cur];
     struct chunk* nx = &p->ch[cur ^ 1];
     int sub_rc = 0, more = issued < n;
+    uint64_t gen;
     oo_rx_poll_stats base;
     if( more ) {
       /* the next chunk's counters start where this one's will end: they
@@ -464,7 +497,23 @@ int oo_rx_poll_evs(oo_rx_poll* p, const oo_rx_poll_ev* evs, uint32_t n,
       k = n - issued < p->cfg.evs_per_poll ? n - issued : p->cfg.evs_per_poll;
       sub_rc = chunk_submit(p, nx, evs + issued, k, &base);
     }
+    gen = oo_gpu_rx_table_gen(p->gpu);
     rc = chunk_complete(p, c, stats);
+    if( rc == 0 && more && sub_rc == 0 && oo_gpu_rx_table_gen(p->gpu) != gen ) {
+      /* This chunk's callbacks changed the tables (a filter inserted on an
+       * accept, removed on a close, next to ci_netif_filter_insert / _remove)
+       * after the next chunk was transformed: the reference loop, one event
+       * after another, would run the next packets on the new tables.  The
+       * next chunk is transformed again (its first transform's records are
+       * discarded; nothing was dispatched from them). */
+      if( nx->busy ) {
+        (void)oo_gpu_rx_wait(p->gpu, nx->ticket);
+        nx->busy = 0;
+      }
+      memset(&base, 0, sizeof(base));
+      sub_rc = chunk_submit(p, nx, evs + issued, k, &base);
+      ++nx->st.n_resubmit;
+    }
     if( rc < 0 ) {
       if( more && sub_rc == 0 && nx->busy ) {  /* it must not outlive the call */
         (void)oo_gpu_rx_wait(p->gpu, nx->ticket);

@@ -173,3 +173,44 @@ def test_poll_counters_match_reference_run(cuda, name):
     assert st["n_pkt_handler"] == int(((c["handled"] == 1) & (c["entry"] == 0)).sum())
     p.close()
     g.close()
+
+
+@pytest.mark.parametrize("evs_per_poll", (16, 64))
+def test_poll_table_change_in_a_callback(cuda, evs_per_poll):
+    """A callback that changes the tables (a filter removed as its socket
+    closes, next to ci_netif_filter_remove) while the next chunk is already
+    transformed: the packets after it see the new tables, as the reference's
+    one-event-at-a-time loop would -- the shim transforms that
+    chunk again."""
+    import cases
+    socks, filters = cases.order_world()
+    g = GpuRxStack(device=0, host_stage_bytes=16 << 20, host_stage_pkts=4096)
+    install(g, (socks, filters))
+    f = cases.order_frame()
+    n = 4 * evs_per_poll
+    pool = np.zeros(n * 2048, np.uint8)
+    evs = np.zeros(n, poll.EV_DTYPE)
+    for i in range(n):
+        pool[i * 2048 + 192:i * 2048 + 192 + len(f)] = np.frombuffer(f, np.uint8)
+        evs[i] = (i, 192, len(f), poll.EV_SOP, 0, 0, 0)
+    cut = evs_per_poll + 3  # inside the second chunk: the third is in flight
+
+    class Closer(Recorder):
+        def post_future(self, i, r, fu):
+            if i == cut:
+                assert g.filter_remove(*filters[0]) == 0  # stage 1's socket closes
+            return super().post_future(i, r, fu)
+
+        def full_handler(self, i, r):
+            if i == cut:
+                assert g.filter_remove(*filters[0]) == 0
+            super().full_handler(i, r)
+
+    rec = Closer()
+    p = poll.RxPoll(g, pool, 2048, evs_per_poll, True, rec)
+    assert p.poll(evs) == n
+    stages = [int(r["stage"]) for r in rec.recs]
+    assert stages == [1] * (cut + 1) + [2] * (n - cut - 1)
+    assert p.stats.n_resubmit == 1
+    p.close()
+    g.close()

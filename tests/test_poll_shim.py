@@ -29,9 +29,9 @@ def test_exports_every_declared_symbol():
 
 
 def test_layouts_match_header():
-    assert ctypes.sizeof(poll.Stats) == 8 * len(poll.STAT_NAMES) == 184
+    assert ctypes.sizeof(poll.Stats) == 8 * len(poll.STAT_NAMES) == 200
     assert ctypes.sizeof(poll.Ops) == 6 * 8
-    assert ctypes.sizeof(poll.PollCfg) == 32
+    assert ctypes.sizeof(poll.PollCfg) == 56
     assert poll.EV_DTYPE.itemsize == 16 and ctypes.sizeof(poll.Future) == 24
 
 

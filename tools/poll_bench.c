@@ -14,8 +14,12 @@
  *   tools/poll_bench <config> <frames> <evs_per_poll> [...]
  *
  * One JSON line per (evs_per_poll, mode); mode: gather (frames copied into
- * the shim's registered buffer) or zero_copy (the pool registered, frames
- * read in place).
+ * the shim's registered buffer), zero_copy (the pool registered, frames
+ * read in place), or zero_copy_crossover (zero copy with
+ * OO_RX_POLL_CROSSOVER: a chunk the cost model prices below the device
+ * batch goes back through other_ev, and this program's other_ev runs the
+ * per-event CPU loop on it inside the timed poll -- the deployed shape).
+ * The last line fits the model's constants to the runs.
  */
 #include <errno.h>
 #include <stdio.h>
@@ -44,14 +48,25 @@ static int cmp_d(const void* a, const void* b)
   return x < y ? -1 : x > y;
 }
 
-struct tally { uint64_t calls; };
+struct tally {
+  uint64_t calls, cpu_events;
+  oo_or_tables* ot;       /* the per-event loop's tables (other_ev)        */
+  const uint8_t* pool;
+};
 static int cb_future(void* a, uint32_t id, const uint8_t* f, const oo_gpu_rx_result* r,
                      const oo_rx_poll_future* fu)
 { (void)id; (void)f; (void)r; (void)fu; ++((struct tally*)a)->calls; return 0; }
 static void cb_h(void* a, uint32_t id, const uint8_t* f, const oo_gpu_rx_result* r)
 { (void)id; (void)f; (void)r; ++((struct tally*)a)->calls; }
+/* An event handed back: the caller's loop transforms it, one at a time. */
 static void cb_other(void* a, const oo_rx_poll_ev* e)
-{ (void)e; ++((struct tally*)a)->calls; }
+{
+  struct tally* t = a;
+  oo_gpu_rx_result r;
+  ++t->calls;
+  ++t->cpu_events;
+  oo_or_rx_one(t->ot, t->pool + (uint64_t)e->rq_id * BUF + e->ofs, e->len, e->intf_i, &r);
+}
 
 int main(int argc, char** argv)
 {
@@ -66,7 +81,7 @@ int main(int argc, char** argv)
   oo_or_tables* ot;
   uint64_t seed, need, pool_bytes;
   uint8_t hw0 = 0;
-  double cpu_ns;
+  double cpu_ns, mean_len = 0;
   if( argc < 4 ) {
     fprintf(stderr, "usage: %s config frames evs_per_poll...\n", argv[0]);
     return 2;
@@ -101,7 +116,9 @@ int main(int argc, char** argv)
     evs[i].len = (uint16_t)len;
     evs[i].flags = OO_RX_EV_SOP;
     evs[i].intf_i = 0;
+    mean_len += len;
   }
+  mean_len /= n;
 
   /* The per-event CPU loop: one frame at a time, one core. */
   ot = oo_or_tables_new(16, 14, 8192, &hw0, 1);
@@ -142,8 +159,8 @@ int main(int argc, char** argv)
   for( k = 3; k < argc; ++k ) {
     uint32_t epp = (uint32_t)atoi(argv[k]);
     int zc;
-    for( zc = 0; zc < 2; ++zc ) {
-      struct tally t = { 0 };
+    for( zc = 0; zc < 3; ++zc ) {
+      struct tally t = { 0, 0, ot, pool };
       oo_rx_poll_ops ops = { cb_future, cb_h, cb_h, cb_h, cb_other, &t };
       oo_rx_poll_cfg pc;
       oo_rx_poll_stats st;
@@ -158,6 +175,8 @@ int main(int argc, char** argv)
       pc.evs_per_poll = epp;
       pc.sw_verify = 1;
       pc.flags = zc ? OO_RX_POLL_ZERO_COPY : 0;
+      if( zc == 2 )
+        pc.flags |= OO_RX_POLL_CROSSOVER;
       if( (rc = oo_rx_poll_open(&p, gpu, &pc, &ops)) != 0 ) {
         fprintf(stderr, "oo_rx_poll_open: %d\n", rc);
         return 5;
@@ -181,11 +200,13 @@ int main(int argc, char** argv)
       printf("{\"config\": %d, \"frames\": %d, \"evs_per_poll\": %u, \"mode\": \"%s\", "
              "\"zero_copy_active\": %d, \"polls\": %u, \"poll_us_median\": %.2f, "
              "\"poll_us_p99\": %.2f, \"mpps\": %.3f, \"cpu_per_event_ns\": %.1f, "
-             "\"cpu_mpps_1core\": %.3f, \"cpu_poll_us_equiv\": %.2f, \"callbacks\": %llu}\n",
-             cfg, n, epp, zc ? "zero_copy" : "gather", oo_rx_poll_zero_copy(p), npoll,
+             "\"cpu_mpps_1core\": %.3f, \"cpu_poll_us_equiv\": %.2f, \"callbacks\": %llu, "
+             "\"handed_back\": %llu, \"mean_len\": %.1f}\n",
+             cfg, n, epp, zc == 2 ? "zero_copy_crossover" : zc ? "zero_copy" : "gather",
+             oo_rx_poll_zero_copy(p), npoll,
              lat[npoll / 2], lat[(npoll * 99) / 100 < npoll ? (npoll * 99) / 100 : npoll - 1],
              n / total, cpu_ns, 1e3 / cpu_ns, cpu_ns * epp * 1e-3,
-             (unsigned long long)t.calls);
+             (unsigned long long)t.calls, (unsigned long long)st.n_handback / 2, mean_len);
       fflush(stdout);
       oo_rx_poll_close(p);
       free(lat);
