@@ -12,7 +12,7 @@ PRODUCT := onload_amd/liboo_gpu_rx.so
 PKTGEN  := onload_amd/liboo_pktgen.so
 SHIM    := onload_amd/liboo_rx_poll.so
 SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_rx_kernel_short.hip onload_amd/csrc/oo_table_kernel.hip \
-           onload_amd/csrc/oo_gpu_rx.cpp onload_amd/csrc/oo_rx_csum.cpp
+           onload_amd/csrc/oo_gpu_rx.cpp onload_amd/csrc/oo_gpu_rx_group.cpp onload_amd/csrc/oo_rx_csum.cpp
 HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 
 # Builds of the same kernels with other ring / extra-round / wave counts
@@ -32,7 +32,7 @@ build/check/liboo_gpu_rx_%.so: $(SRCS) $(HDRS)
 COMMA := ,
 
 $(PRODUCT): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,liboo_gpu_rx.so -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,liboo_gpu_rx.so -o $@ $(SRCS) -ldl
 
 # The batched ci_netif_poll_evq RX branch (plain C over the C ABI).
 $(SHIM): src/shim/oo_rx_poll.c include/oo_rx_poll.h include/oo_gpu_rx.h $(PRODUCT)

@@ -375,6 +375,92 @@ int oo_gpu_rx_batch(oo_gpu_rx_ctx* ctx, const void* frames,
                     oo_gpu_rx_counters* delta);
 
 /* ---------------------------------------------------------------------
+ * Multi-GPU group (SURVEY.md §8(b) "device ids", §8(e)).  Packets are
+ * independent and the tables are read-only during a batch, so one stack's
+ * batches spread over the GPUs of a node as contiguous shares, one per
+ * member; every member holds a replica of the tables, kept identical by
+ * applying the same changes in the same order (deterministic placement,
+ * return codes included -- oof's single serialisation point,
+ * oof_interface.c:184-217); no collective touches the data path.
+ *
+ * Two shapes.  In one process: oo_gpu_rx_group_open over a device list (a
+ * device may repeat, several members on one GPU; a negative device makes a
+ * host-only member), the calling thread driving every member.  Across
+ * processes, one per GPU: rank 0 makes an id (oo_gpu_rx_group_rccl_id), the
+ * caller's control plane hands its OO_GPU_RX_GROUP_ID_BYTES to every rank,
+ * each joins with its rank (one local member on cfg->device) and RCCL over
+ * xGMI carries the table image, the changes and the records (librccl is
+ * loaded at the first join: -ENOSYS without it).
+ * --------------------------------------------------------------------- */
+#define OO_GPU_RX_GROUP_ID_BYTES 128
+
+typedef struct oo_gpu_rx_group oo_gpu_rx_group;
+
+/* One member's share of a batch: its frames, descriptors, records and
+ * (optional) counters in its device's memory, and its stream. */
+typedef struct oo_gpu_rx_shard {
+  const void*             d_frames;
+  uint64_t                frames_bytes;
+  const oo_gpu_pkt_desc*  d_desc;
+  uint32_t                n;
+  uint32_t                rsvd;
+  oo_gpu_rx_result*       d_out;
+  oo_gpu_rx_counters*     d_counters;   /* may be NULL */
+  void*                   stream;
+} oo_gpu_rx_shard;
+
+/* n members (<= 64), member i a context opened with cfg on devices[i]. */
+int  oo_gpu_rx_group_open(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg,
+                          const int32_t* devices, uint32_t n);
+int  oo_gpu_rx_group_rccl_id(void* id);
+int  oo_gpu_rx_group_join(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32_t rank,
+                          uint32_t nranks, const void* id);
+void oo_gpu_rx_group_close(oo_gpu_rx_group* g);
+/* Local members, this process's rank (0 in one process), member i's context
+ * (its own calls -- export, sync_tables, stream_done -- work as for any
+ * context; table changes go through the group). */
+uint32_t       oo_gpu_rx_group_size(const oo_gpu_rx_group* g);
+uint32_t       oo_gpu_rx_group_rank(const oo_gpu_rx_group* g);
+oo_gpu_rx_ctx* oo_gpu_rx_group_member(oo_gpu_rx_group* g, uint32_t i);
+/* Table changes on every local member in call order; the members' common
+ * return code (-EIO if a replica disagrees).  Across processes only rank 0
+ * changes the tables (-EPERM elsewhere); the changes reach the other ranks
+ * with oo_gpu_rx_group_share_ops. */
+int oo_gpu_rx_group_table_insert(oo_gpu_rx_group* g, int af, const void* laddr,
+                                 uint16_t lport_be16, const void* raddr, uint16_t rport_be16,
+                                 uint8_t protocol, int32_t sock_id);
+int oo_gpu_rx_group_table_remove(oo_gpu_rx_group* g, int af, const void* laddr,
+                                 uint16_t lport_be16, const void* raddr, uint16_t rport_be16,
+                                 uint8_t protocol, int32_t sock_id);
+int oo_gpu_rx_group_sock_set(oo_gpu_rx_group* g, int32_t sock_id, const oo_gpu_rx_sock* sock);
+/* Byte-balanced contiguous split of n packets (host descriptors) into
+ * `parts` shares: first[0..parts], share k = [first[k], first[k+1]), each
+ * holding about the same algorithmic bytes (frame + 16-B descriptor + 32-B
+ * record). */
+int oo_gpu_rx_group_split(const oo_gpu_rx_group* g, const oo_gpu_pkt_desc* desc, uint32_t n,
+                          uint32_t parts, uint32_t* first);
+/* In one process: member i transforms shards[i], asynchronously on its
+ * stream (oo_gpu_rx_process_dev). */
+int oo_gpu_rx_group_process(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards);
+/* In one process, after process: the members' records into dst (sum of
+ * the shards' n, member order; device or host memory, NULL: none), each
+ * copied on its member's stream; then waits for every member and sums the
+ * counters into *counters (host, may be NULL). */
+int oo_gpu_rx_group_gather(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards,
+                           oo_gpu_rx_result* dst, oo_gpu_rx_counters* counters);
+/* Across processes (every rank calls each, collectively): rank 0's tables
+ * to every rank (one image broadcast); rank 0's changes since then, applied
+ * by the others in order (returns how many); every rank's n records to
+ * rank 0's d_dst in rank order (rank 0 passes counts[nranks]); the device
+ * counters summed on every rank. */
+int oo_gpu_rx_group_share_tables(oo_gpu_rx_group* g, void* stream);
+int oo_gpu_rx_group_share_ops(oo_gpu_rx_group* g, void* stream);
+int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_out, uint32_t n,
+                                oo_gpu_rx_result* d_dst, const uint32_t* counts, void* stream);
+int oo_gpu_rx_group_sum_counters(oo_gpu_rx_group* g, oo_gpu_rx_counters* d_counters,
+                                 void* stream);
+
+/* ---------------------------------------------------------------------
  * Host-pure checksum verifiers: the reference's public C API for this path
  * (src/include/etherfabric/checksum.h:246-308, src/lib/ciul/checksum.c:
  * 298-351) and ci_ip_csum_correct (netif_event.c:80-94), same argument

@@ -1,0 +1,448 @@
+// SPDX-License-Identifier: BSD-2-Clause
+//
+// oo_gpu_rx_group.cpp -- the multi-GPU form of the C ABI (include/oo_gpu_rx.h
+// "Multi-GPU group"; SURVEY.md §8(b) "device ids", §8(e)).
+//
+// Packets are independent and the filter tables are read-only during a
+// batch, so a stack's batches spread over the GPUs of one node as
+// contiguous shares, one per member, with a replica of the tables on every
+// member and no collective on the data path.  What moves between members:
+//  * table changes -- every replica applies the same ops in the same order
+//    (the mirror's and the device's placement are deterministic, so the
+//    replicas stay byte-identical, return codes included: oof applies its
+//    deferred ops at one serialisation point the same way,
+//    oof_interface.c:184-217);
+//  * the records, gathered into one array after a batch, and the counters,
+//    summed.
+// Two shapes:
+//  * in one process (oo_gpu_rx_group_open): members on a list of devices
+//    (a device may repeat), driven by the calling thread -- Onload's stack
+//    lives in one process;
+//  * across processes, one per GPU (oo_gpu_rx_group_join): this process's
+//    one member, RCCL over xGMI between the ranks (librccl, loaded when the
+//    first group joins) for the table image, the ops and the records.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+#include <errno.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "oo_rx_device.h"
+
+namespace {
+
+// librccl entry points (dlopen: the library is needed only by a group that
+// joins across processes).
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*get_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*bcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
+                        hipStream_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*allreduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*group_start)(void) = nullptr;
+  ncclResult_t (*group_end)(void) = nullptr;
+};
+
+Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (tried) return r.h ? &r : nullptr;
+  tried = true;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (h == nullptr) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (h == nullptr) return nullptr;
+  bool ok = true;
+  auto sym = [&](auto& fn, const char* name) {
+    fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+    ok = ok && fn != nullptr;
+  };
+  sym(r.get_id, "ncclGetUniqueId");
+  sym(r.init_rank, "ncclCommInitRank");
+  sym(r.destroy, "ncclCommDestroy");
+  sym(r.bcast, "ncclBroadcast");
+  sym(r.send, "ncclSend");
+  sym(r.recv, "ncclRecv");
+  sym(r.allreduce, "ncclAllReduce");
+  sym(r.group_start, "ncclGroupStart");
+  sym(r.group_end, "ncclGroupEnd");
+  if (!ok) {
+    dlclose(h);
+    return nullptr;
+  }
+  r.h = h;
+  return &r;
+}
+
+// One table change as it travels to the other ranks (join shape): the
+// arguments of oo_gpu_rx_table_insert / _remove / oo_gpu_rx_sock_set.
+// 96 B.
+struct GroupOp {
+  uint8_t kind;  // 1 insert, 2 remove, 3 socket
+  uint8_t af, proto, raddr_any;
+  uint16_t lport, rport;
+  int32_t sock;
+  uint32_t rsvd;
+  uint8_t laddr[16], raddr[16];
+  oo_gpu_rx_sock s;
+};
+static_assert(sizeof(GroupOp) == 96, "group op layout");
+
+}  // namespace
+
+struct oo_gpu_rx_group {
+  std::vector<oo_gpu_rx_ctx*> m;  // local members
+  std::vector<int32_t> dev;       // their devices
+  // join shape
+  uint32_t rank = 0, nranks = 1;
+  ncclComm_t comm = nullptr;
+  std::vector<GroupOp> ops;       // rank 0's changes since the last share_ops
+  void* d_ops = nullptr;          // device staging for the op broadcast
+  uint64_t d_ops_cap = 0;
+  void* d_img = nullptr;          // device staging for the table image
+};
+
+namespace {
+
+int apply_op(oo_gpu_rx_ctx* c, const GroupOp& o) {
+  const void* ra = o.raddr_any ? nullptr : o.raddr;
+  switch (o.kind) {
+    case 1: return oo_gpu_rx_table_insert(c, o.af, o.laddr, o.lport, ra, o.rport, o.proto, o.sock);
+    case 2: return oo_gpu_rx_table_remove(c, o.af, o.laddr, o.lport, ra, o.rport, o.proto, o.sock);
+    case 3: return oo_gpu_rx_sock_set(c, o.sock, &o.s);
+    default: return -EINVAL;
+  }
+}
+
+// Applies one change to every local member in order (and queues it for
+// the other ranks in the join shape): the first member's return code; the
+// replicas agree, and a member that does not is reported as -EIO.
+int group_change(oo_gpu_rx_group* g, const GroupOp& o) {
+  if (g->m.empty()) return -EINVAL;
+  if (g->nranks > 1 && g->rank != 0) return -EPERM;  // rank 0 owns the tables
+  const int rc = apply_op(g->m[0], o);
+  for (size_t i = 1; i < g->m.size(); ++i)
+    if (apply_op(g->m[i], o) != rc) return -EIO;
+  if (g->nranks > 1 && g->rank == 0) {
+    try {
+      g->ops.push_back(o);
+    } catch (...) {
+      return -ENOMEM;
+    }
+  }
+  return rc;
+}
+
+GroupOp tuple_change(uint8_t kind, int af, const void* laddr, uint16_t lport, const void* raddr,
+                     uint16_t rport, uint8_t proto, int32_t id) {
+  GroupOp o;
+  memset(&o, 0, sizeof(o));
+  o.kind = kind;
+  o.af = (uint8_t)af;
+  o.proto = proto;
+  o.lport = lport;
+  o.rport = rport;
+  o.sock = id;
+  const size_t n = af == 6 ? 16 : 4;
+  if (laddr) memcpy(o.laddr, laddr, n);
+  if (raddr) memcpy(o.raddr, raddr, n);
+  else o.raddr_any = 1;
+  return o;
+}
+
+void group_free(oo_gpu_rx_group* g) {
+  for (oo_gpu_rx_ctx* c : g->m) oo_gpu_rx_close(c);
+  if (g->d_ops) (void)hipFree(g->d_ops);
+  if (g->d_img) (void)hipFree(g->d_img);
+  if (g->comm) {
+    Rccl* r = rccl();
+    if (r) (void)r->destroy(g->comm);
+  }
+  delete g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oo_gpu_rx_group_open(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, const int32_t* devices,
+                         uint32_t n) {
+  if (out == nullptr || cfg == nullptr || devices == nullptr || n == 0 || n > 64) return -EINVAL;
+  *out = nullptr;
+  oo_gpu_rx_group* g = new (std::nothrow) oo_gpu_rx_group();
+  if (g == nullptr) return -ENOMEM;
+  try {
+    for (uint32_t i = 0; i < n; ++i) {
+      oo_gpu_rx_cfg c = *cfg;
+      c.device = devices[i];
+      oo_gpu_rx_ctx* ctx = nullptr;
+      const int rc = oo_gpu_rx_open(&ctx, &c);
+      if (rc != 0) {
+        group_free(g);
+        return rc;
+      }
+      g->m.push_back(ctx);
+      g->dev.push_back(devices[i]);
+    }
+  } catch (...) {
+    group_free(g);
+    return -ENOMEM;
+  }
+  *out = g;
+  return 0;
+}
+
+int oo_gpu_rx_group_rccl_id(void* id) {
+  if (id == nullptr) return -EINVAL;
+  Rccl* r = rccl();
+  if (r == nullptr) return -ENOSYS;
+  ncclUniqueId u;
+  if (r->get_id(&u) != ncclSuccess) return -EIO;
+  static_assert(sizeof(u) == OO_GPU_RX_GROUP_ID_BYTES, "RCCL unique id size");
+  memcpy(id, &u, sizeof(u));
+  return 0;
+}
+
+int oo_gpu_rx_group_join(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32_t rank,
+                         uint32_t nranks, const void* id) {
+  if (out == nullptr || cfg == nullptr || id == nullptr || nranks == 0 || rank >= nranks ||
+      cfg->device < 0)
+    return -EINVAL;
+  *out = nullptr;
+  Rccl* r = rccl();
+  if (r == nullptr) return -ENOSYS;
+  oo_gpu_rx_group* g = nullptr;
+  int rc = oo_gpu_rx_group_open(&g, cfg, &cfg->device, 1);
+  if (rc != 0) return rc;
+  g->rank = rank;
+  g->nranks = nranks;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  if (hipSetDevice(cfg->device) != hipSuccess || r->init_rank(&g->comm, (int)nranks, u, (int)rank) != ncclSuccess) {
+    g->comm = nullptr;
+    group_free(g);
+    return -EIO;
+  }
+  *out = g;
+  return 0;
+}
+
+void oo_gpu_rx_group_close(oo_gpu_rx_group* g) {
+  if (g) group_free(g);
+}
+
+uint32_t oo_gpu_rx_group_size(const oo_gpu_rx_group* g) { return g ? (uint32_t)g->m.size() : 0; }
+
+uint32_t oo_gpu_rx_group_rank(const oo_gpu_rx_group* g) { return g ? g->rank : 0; }
+
+oo_gpu_rx_ctx* oo_gpu_rx_group_member(oo_gpu_rx_group* g, uint32_t i) {
+  return (g && i < g->m.size()) ? g->m[i] : nullptr;
+}
+
+int oo_gpu_rx_group_table_insert(oo_gpu_rx_group* g, int af, const void* laddr, uint16_t lport,
+                                 const void* raddr, uint16_t rport, uint8_t proto, int32_t id) {
+  if (g == nullptr || laddr == nullptr || (af != 4 && af != 6)) return -EINVAL;
+  return group_change(g, tuple_change(1, af, laddr, lport, raddr, rport, proto, id));
+}
+
+int oo_gpu_rx_group_table_remove(oo_gpu_rx_group* g, int af, const void* laddr, uint16_t lport,
+                                 const void* raddr, uint16_t rport, uint8_t proto, int32_t id) {
+  if (g == nullptr || laddr == nullptr || (af != 4 && af != 6)) return -EINVAL;
+  return group_change(g, tuple_change(2, af, laddr, lport, raddr, rport, proto, id));
+}
+
+int oo_gpu_rx_group_sock_set(oo_gpu_rx_group* g, int32_t id, const oo_gpu_rx_sock* s) {
+  if (g == nullptr || s == nullptr) return -EINVAL;
+  GroupOp o;
+  memset(&o, 0, sizeof(o));
+  o.kind = 3;
+  o.sock = id;
+  o.s = *s;
+  return group_change(g, o);
+}
+
+int oo_gpu_rx_group_split(const oo_gpu_rx_group* g, const oo_gpu_pkt_desc* desc, uint32_t n,
+                          uint32_t parts, uint32_t* first) {
+  if (g == nullptr || first == nullptr || parts == 0 || (n > 0 && desc == nullptr)) return -EINVAL;
+  // The algorithmic bytes of a packet: its frame, its descriptor and its
+  // record (DESIGN.md §2 "Rooflines"); every share gets about total / parts.
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) total += (uint64_t)desc[i].len + 48u;
+  first[0] = 0;
+  uint64_t acc = 0;
+  uint32_t k = 1;
+  for (uint32_t i = 0; i < n && k < parts; ++i) {
+    acc += (uint64_t)desc[i].len + 48u;
+    while (k < parts && acc * parts >= total * k) first[k++] = i + 1;
+  }
+  while (k <= parts) first[k++] = n;
+  return 0;
+}
+
+int oo_gpu_rx_group_process(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards) {
+  if (g == nullptr || shards == nullptr) return -EINVAL;
+  for (size_t i = 0; i < g->m.size(); ++i) {
+    const oo_gpu_rx_shard& s = shards[i];
+    const int rc = oo_gpu_rx_process_dev(g->m[i], s.d_frames, s.frames_bytes, s.d_desc, s.n,
+                                         s.d_out, s.d_counters, s.stream);
+    if (rc != 0) return rc;
+  }
+  return 0;
+}
+
+int oo_gpu_rx_group_gather(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards,
+                           oo_gpu_rx_result* dst, oo_gpu_rx_counters* counters) {
+  if (g == nullptr || shards == nullptr) return -EINVAL;
+  uint64_t at = 0;
+  for (size_t i = 0; i < g->m.size(); ++i) {
+    const oo_gpu_rx_shard& s = shards[i];
+    if (g->dev[i] < 0 || hipSetDevice(g->dev[i]) != hipSuccess) return -ENODEV;
+    hipStream_t st = static_cast<hipStream_t>(s.stream);
+    if (dst != nullptr && s.n > 0 &&
+        hipMemcpyAsync(dst + at, s.d_out, sizeof(oo_gpu_rx_result) * s.n, hipMemcpyDefault, st) !=
+            hipSuccess)
+      return -EIO;
+    at += s.n;
+  }
+  if (counters != nullptr) memset(counters, 0, sizeof(*counters));
+  for (size_t i = 0; i < g->m.size(); ++i) {
+    const oo_gpu_rx_shard& s = shards[i];
+    if (hipSetDevice(g->dev[i]) != hipSuccess ||
+        hipStreamSynchronize(static_cast<hipStream_t>(s.stream)) != hipSuccess)
+      return -EIO;
+    if (counters != nullptr && s.d_counters != nullptr) {
+      oo_gpu_rx_counters c;
+      if (hipMemcpy(&c, s.d_counters, sizeof(c), hipMemcpyDefault) != hipSuccess) return -EIO;
+      for (int k = 0; k < OO_RX_R_COUNT; ++k) counters->by_reason[k] += c.by_reason[k];
+    }
+  }
+  return 0;
+}
+
+int oo_gpu_rx_group_share_tables(oo_gpu_rx_group* g, void* stream) {
+  if (g == nullptr || g->m.size() != 1) return -EINVAL;
+  if (g->nranks == 1) return 0;
+  Rccl* r = rccl();
+  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
+  oo_gpu_rx_ctx* c = g->m[0];
+  const uint64_t bytes = oo_gpu_rx_table_image_bytes(c);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
+  if (g->d_img == nullptr && hipMalloc(&g->d_img, bytes) != hipSuccess) return -ENOMEM;
+  int rc = 0;
+  if (g->rank == 0) rc = oo_gpu_rx_table_export(c, g->d_img, bytes, stream);
+  if (rc != 0) return rc;
+  if (r->bcast(g->d_img, g->d_img, bytes, ncclUint8, 0, g->comm, s) != ncclSuccess) return -EIO;
+  if (g->rank != 0) rc = oo_gpu_rx_table_import(c, g->d_img, bytes, stream);
+  g->ops.clear();  // rank 0's changes so far are in the image
+  return rc;
+}
+
+int oo_gpu_rx_group_share_ops(oo_gpu_rx_group* g, void* stream) {
+  if (g == nullptr || g->m.size() != 1) return -EINVAL;
+  if (g->nranks == 1) return 0;
+  Rccl* r = rccl();
+  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
+  // The count, then the ops (96 B each), from rank 0.
+  uint64_t cnt = g->rank == 0 ? g->ops.size() : 0;
+  const uint64_t need = sizeof(uint64_t) + sizeof(GroupOp) * std::max<uint64_t>(cnt, 1);
+  if (g->d_ops_cap < need) {
+    if (g->d_ops) (void)hipFree(g->d_ops);
+    g->d_ops = nullptr;
+    g->d_ops_cap = 0;
+  }
+  if (g->d_ops == nullptr) {
+    const uint64_t cap = std::max<uint64_t>(need, 1u << 20);
+    if (hipMalloc(&g->d_ops, cap) != hipSuccess) return -ENOMEM;
+    g->d_ops_cap = cap;
+  }
+  if (g->rank == 0 &&
+      hipMemcpyAsync(g->d_ops, &cnt, sizeof(cnt), hipMemcpyHostToDevice, s) != hipSuccess)
+    return -EIO;
+  if (r->bcast(g->d_ops, g->d_ops, sizeof(cnt), ncclUint8, 0, g->comm, s) != ncclSuccess ||
+      hipMemcpyAsync(&cnt, g->d_ops, sizeof(cnt), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return -EIO;
+  if (cnt == 0) return 0;
+  if (sizeof(uint64_t) + sizeof(GroupOp) * cnt > g->d_ops_cap) return -ENOMEM;  // (the others' buffer)
+  uint8_t* body = static_cast<uint8_t*>(g->d_ops) + sizeof(uint64_t);
+  std::vector<GroupOp> in;
+  try {
+    in.resize(cnt);
+  } catch (...) {
+    return -ENOMEM;
+  }
+  if (g->rank == 0 &&
+      hipMemcpyAsync(body, g->ops.data(), sizeof(GroupOp) * cnt, hipMemcpyHostToDevice, s) !=
+          hipSuccess)
+    return -EIO;
+  if (r->bcast(body, body, sizeof(GroupOp) * cnt, ncclUint8, 0, g->comm, s) != ncclSuccess ||
+      hipMemcpyAsync(in.data(), body, sizeof(GroupOp) * cnt, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return -EIO;
+  if (g->rank != 0)
+    for (const GroupOp& o : in) (void)apply_op(g->m[0], o);  // rank 0 applied them at its calls
+  g->ops.clear();
+  return (int)cnt;
+}
+
+int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_out, uint32_t n,
+                                oo_gpu_rx_result* d_dst, const uint32_t* counts, void* stream) {
+  if (g == nullptr || g->m.size() != 1 || (n > 0 && d_out == nullptr)) return -EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
+  if (g->nranks == 1) {
+    if (d_dst != nullptr && n > 0 && d_dst != d_out &&
+        hipMemcpyAsync(d_dst, d_out, sizeof(oo_gpu_rx_result) * n, hipMemcpyDefault, s) != hipSuccess)
+      return -EIO;
+    return 0;
+  }
+  Rccl* r = rccl();
+  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
+  if (g->rank == 0 && (d_dst == nullptr || counts == nullptr)) return -EINVAL;
+  if (r->group_start() != ncclSuccess) return -EIO;
+  ncclResult_t e = ncclSuccess;
+  if (g->rank == 0) {
+    uint64_t at = 0;
+    for (uint32_t k = 0; k < g->nranks; ++k) {
+      const uint64_t bytes = sizeof(oo_gpu_rx_result) * (uint64_t)counts[k];
+      if (k == 0) {
+        if (bytes && d_dst != d_out &&
+            hipMemcpyAsync(d_dst, d_out, bytes, hipMemcpyDefault, s) != hipSuccess)
+          e = ncclSystemError;
+      } else if (bytes && e == ncclSuccess) {
+        e = r->recv(reinterpret_cast<uint8_t*>(d_dst) + at, bytes, ncclUint8, (int)k, g->comm, s);
+      }
+      at += bytes;
+    }
+  } else if (n > 0) {
+    e = r->send(d_out, sizeof(oo_gpu_rx_result) * (uint64_t)n, ncclUint8, 0, g->comm, s);
+  }
+  const ncclResult_t e2 = r->group_end();
+  return (e == ncclSuccess && e2 == ncclSuccess) ? 0 : -EIO;
+}
+
+int oo_gpu_rx_group_sum_counters(oo_gpu_rx_group* g, oo_gpu_rx_counters* d_counters, void* stream) {
+  if (g == nullptr || g->m.size() != 1 || d_counters == nullptr) return -EINVAL;
+  if (g->nranks == 1) return 0;
+  Rccl* r = rccl();
+  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
+  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
+  return r->allreduce(d_counters, d_counters, OO_RX_R_COUNT, ncclUint32, ncclSum, g->comm,
+                      static_cast<hipStream_t>(stream)) == ncclSuccess
+             ? 0
+             : -EIO;
+}
+
+}  // extern "C"

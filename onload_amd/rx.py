@@ -79,8 +79,24 @@ class GpuRxStack:
         self.host_stage_bytes = host_stage_bytes
         self.host_stage_pkts = host_stage_pkts
 
+    @classmethod
+    def wrap(cls, ctx, device: int, max_socks: int, lib) -> "GpuRxStack":
+        """A view of a context another object owns (a group member): its
+        calls work as for any stack; closing it is the owner's."""
+        self = cls.__new__(cls)
+        self._lib = lib
+        self._ctx = ctypes.c_void_p(ctx)
+        self._owned = False
+        self.device = device
+        self.max_socks = max_socks
+        self.host_stage_bytes = self.host_stage_pkts = 0
+        return self
+
     # -- lifetime -------------------------------------------------------
     def close(self) -> None:
+        if not getattr(self, "_owned", True):
+            self._ctx = None
+            return
         if self._ctx:
             self._lib.oo_gpu_rx_close(self._ctx)
             self._ctx = None
