@@ -207,20 +207,47 @@ def run_rank(args) -> None:
     log(f"[rank {rank}] packets [{first}, {first + n}) ({buf.nbytes / 1e9:.2f} GB) "
         f"generated in {time.time() - t0:.1f}s")
 
-    stack = GpuRxStack(device=local)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     table_bcast = None
+    group = None
+    group_path = None
     if world > 1:
-        # Rank 0 owns the socket world; the others receive its table image.
+        # The library's multi-GPU group across processes (include/oo_gpu_rx.h
+        # "Multi-GPU group"): rank 0 makes the RCCL id, torch.distributed's
+        # control plane hands it out, every rank joins with one member on its
+        # GPU; rank 0 owns the socket world and the group broadcasts its
+        # table image over RCCL.  Where the join is refused (RCCL takes one
+        # rank per GPU: the shared-GPU rehearsal) the Python path over
+        # torch.distributed does the same, and the line says which ran.
+        from onload_amd.group import GpuRxGroup
+        gid = [GpuRxGroup.rccl_id() if rank == 0 else None]
+        dist.broadcast_object_list(gid, src=0)
+        try:
+            group = GpuRxGroup.join(local, rank, world, gid[0])
+        except OSError as e:
+            log(f"[rank {rank}] group join refused ({e}); torch.distributed path")
+        ok = torch.tensor([1 if group is not None else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and group is not None:
+            group.close()
+            group = None
+        group_path = "c_group_rccl" if group is not None else "torch_distributed"
+        stack = group.members[0] if group is not None else GpuRxStack(device=local)
         if rank == 0:
-            stack.load_world(filters, socks)
+            (group or stack).load_world(filters, socks)
         dist.barrier()
         tb = time.perf_counter()
-        nbytes = shards.broadcast_tables(stack, torch, dist, dev, 0, sh)
+        if group is not None:
+            group.share_tables(sh)
+            nbytes = stack.image_bytes()
+        else:
+            nbytes = shards.broadcast_tables(stack, torch, dist, dev, 0, sh)
         torch.cuda.synchronize(dev)
-        table_bcast = {"bytes": nbytes, "ms": round((time.perf_counter() - tb) * 1e3, 3)}
+        table_bcast = {"bytes": nbytes, "ms": round((time.perf_counter() - tb) * 1e3, 3),
+                       "path": group_path}
     else:
+        stack = GpuRxStack(device=local)
         stack.load_world(filters, socks)
     frames = torch.from_numpy(buf).to(dev)
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
@@ -289,15 +316,26 @@ def run_rank(args) -> None:
     torch.cuda.synchronize(dev)
     gather = None
     if world > 1:
-        dist.all_reduce(ctr)
         tg = time.perf_counter()
-        recs = shards.gather_records(out, n, torch, dist, 0)
+        if group is not None:
+            group.sum_counters(ctr.data_ptr(), sh)
+            cnts = torch.tensor([n], dtype=torch.int64, device=dev)
+            allc = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+            dist.all_gather(allc, cnts)
+            counts_r = [int(c.item()) for c in allc]
+            recs = (torch.empty(sum(counts_r) * RESULT_B, dtype=torch.uint8, device=dev)
+                    if rank == 0 else None)
+            group.gather_rccl(out.data_ptr(), n, recs.data_ptr() if rank == 0 else 0,
+                              counts_r if rank == 0 else None, sh)
+        else:
+            dist.all_reduce(ctr)
+            recs = shards.gather_records(out, n, torch, dist, 0)
         torch.cuda.synchronize(dev)
         if rank == 0:
             r = recs.view(-1, RESULT_B)[:, 0].cpu().numpy()
             ok = bool((np.bincount(r, minlength=32) == ctr.cpu().numpy()).all())
             gather = {"records": int(len(r)), "ms": round((time.perf_counter() - tg) * 1e3, 3),
-                      "counts_match": ok}
+                      "counts_match": ok, "path": group_path}
     counts = ctr.cpu().numpy()
     assert counts.sum() == n_total, counts
 
@@ -392,6 +430,8 @@ def run_rank(args) -> None:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
+        if group is not None:
+            group.close()
         dist.destroy_process_group()
 
 
@@ -593,6 +633,7 @@ def time_pipelined(torch, stack, frames, d_desc, n, mean_len, out, dev, stream, 
     torch.cuda.synchronize(dev)
     ms = float(ev0.elapsed_time(ev1)) / steps
     gbs = (mean_len + DESC_B + RESULT_B) * n / (ms * 1e-3) / 1e9
+    stack.stream_done(s2.cuda_stream)  # the context stops tracking s2 before it goes
     return {"ms_per_batch": round(ms, 5), "mpps": round(n / (ms * 1e-3) / 1e6, 2),
             "achieved_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "streams": 2}
 

@@ -1317,9 +1317,13 @@ int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
     // No batch may still read it.
     for (HostSlot& s : c->slot)
       if (s.busy) (void)hipEventSynchronize(s.done);
+    // Only a stream that launched since its event was last recorded gets a
+    // new one (it may since have been destroyed by a caller that did not
+    // call oo_gpu_rx_stream_done); the others' events already
+    // cover all their work.
     for (Tracked& t : c->track) {
       if (!t.used) continue;
-      hipEvent_t e = mark(t);
+      hipEvent_t e = t.live ? mark(t) : t.ev;
       if (e != nullptr) (void)hipEventSynchronize(e);
     }
     (void)hipHostUnregister(p);
