@@ -269,6 +269,27 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* ctx, const void* src, uint64_t bytes,
  * 0 or -EINVAL. */
 int oo_gpu_rx_set_len_hint(oo_gpu_rx_ctx* ctx, uint32_t mean_frame_len);
 
+/* Launch settings, for measurements: which kernels transform a batch and
+ * how its work is cut.  Results are identical under every setting; the
+ * defaults (all fields 0, gshift -1; or t = NULL) are what DESIGN.md §2
+ * measured fastest.  The library reads no environment: a deployment gets
+ * exactly these defaults unless it calls this.  0 or -EINVAL. */
+typedef struct oo_gpu_rx_tuning {
+  uint32_t path;           /* 0 auto; 1 one rx_kernel launch, 4-slot body ring;
+                              2 the same with the 2-slot ring; 3 the split
+                              transform (win_kernel + body_kernel)            */
+  uint32_t grid_pct;       /* % of the resident grid to launch (0: 100)       */
+  uint32_t groups;         /* tile-claim groups at most (0: by frame size)    */
+  int32_t  gshift;         /* a group's wave runs, log2 (-1: by frame size)   */
+  uint32_t static_tiles;   /* 1: a static tile partition, no claims           */
+  uint32_t tail_tile;      /* packets per tile at the batch's end (0: 32)     */
+  uint32_t tail_per_wave;  /* such tiles per wave (0: 1)                      */
+  uint32_t tstep;          /* static partition tile-size step: 1, else 8      */
+  uint32_t body_bpc;       /* body_kernel blocks per CU at most (0: all that fit) */
+  uint32_t body_tail;      /* body_kernel unit at the batch's end, packets (0: 16) */
+} oo_gpu_rx_tuning;
+int oo_gpu_rx_set_tuning(oo_gpu_rx_ctx* ctx, const oo_gpu_rx_tuning* t);
+
 /* Device-resident batch: frames, descriptors and results all in HBM.
  * Enqueues the transform of n frames on `stream` and returns immediately.
  * d_counters (device, may be NULL) is incremented per reason.

@@ -69,6 +69,35 @@ class Cfg(ctypes.Structure):
 assert ctypes.sizeof(Sock) == 48
 
 
+class Tuning(ctypes.Structure):
+    """oo_gpu_rx_tuning (launch settings, results unchanged)."""
+    _fields_ = [("path", ctypes.c_uint32), ("grid_pct", ctypes.c_uint32),
+                ("groups", ctypes.c_uint32), ("gshift", ctypes.c_int32),
+                ("static_tiles", ctypes.c_uint32), ("tail_tile", ctypes.c_uint32),
+                ("tail_per_wave", ctypes.c_uint32), ("tstep", ctypes.c_uint32),
+                ("body_bpc", ctypes.c_uint32), ("body_tail", ctypes.c_uint32)]
+
+
+#: The measurement settings tests and tools pass through the environment of
+#: the *Python* process (the C library reads none): variable -> field.
+TUNING_ENV = {"OO_RX_KERNEL": "path", "OO_RX_GRID_PCT": "grid_pct", "OO_RX_GROUPS": "groups",
+              "OO_RX_GSHIFT": "gshift", "OO_RX_STATIC": "static_tiles",
+              "OO_RX_TAIL_TILE": "tail_tile", "OO_RX_TAIL_PER_WAVE": "tail_per_wave",
+              "OO_RX_TSTEP": "tstep", "OO_RX_BODY_BPC": "body_bpc", "OO_RX_BODY_TAIL": "body_tail"}
+
+
+def tuning_from_env() -> "Tuning | None":
+    t = Tuning()
+    t.gshift = -1
+    seen = False
+    for var, field in TUNING_ENV.items():
+        v = os.environ.get(var)
+        if v:
+            setattr(t, field, int(v, 0))
+            seen = True
+    return t if seen else None
+
+
 class PgFilter(ctypes.Structure):
     """oo_pg_filter (onload_amd/csrc/oo_pktgen.h)."""
     _fields_ = [("sock", ctypes.c_int32), ("af", ctypes.c_uint8), ("proto", ctypes.c_uint8),
@@ -126,6 +155,7 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_stream_done": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_table_gen": (ctypes.c_uint64, [_P]),
     "oo_gpu_rx_set_len_hint": (ctypes.c_int, [_P, _U32]),
+    "oo_gpu_rx_set_tuning": (ctypes.c_int, [_P, ctypes.POINTER(Tuning)]),
     "oo_gpu_rx_process_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _P]),
     "oo_gpu_tx_fill_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P]),
     "oo_gpu_rx_xdp_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _U32, _U32, ctypes.c_int,

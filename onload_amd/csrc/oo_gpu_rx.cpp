@@ -68,10 +68,6 @@ using oo_rx::ST_REHASHED;
 using oo_rx::ST_TOMBSTONE;
 using oo_rx::TableOp;
 
-uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
-}
 
 inline uint32_t ld32(const void* p) {
   uint32_t v;
@@ -211,6 +207,7 @@ struct oo_gpu_rx_ctx {
   uint32_t gshift = ~0u;       // claim group of a wave: (gwave >> gshift) mod groups (~0u: per launch)
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t grid_short = 0;     // resident blocks of the short-frame rx_kernel (0: unused)
+  uint32_t ncu = 0, bpc[4] = {0, 0, 0, 0};  // CUs; resident blocks per CU of the four kernels
   uint32_t grid_win = 0;       // resident blocks of win_kernel (split transform)
   uint32_t grid_body = 0;      // resident blocks of body_kernel
   uint32_t body_tail = 16;     // packets per body_kernel unit at the batch's end
@@ -728,11 +725,41 @@ int alloc_host_slots(oo_gpu_rx_ctx* c) {
   return 0;
 }
 
+// The launch settings (oo_gpu_rx_set_tuning; nullptr: the defaults).
+void apply_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
+  oo_gpu_rx_tuning d;
+  memset(&d, 0, sizeof(d));
+  d.gshift = -1;
+  if (t == nullptr) t = &d;
+  const uint32_t pct = t->grid_pct ? t->grid_pct : 100u;
+  auto grid = [&](uint32_t bpc) {
+    return bpc ? std::max<uint32_t>(1, bpc * c->ncu * pct / 100u) : 0u;
+  };
+  c->grid = std::max<uint32_t>(1, grid(c->bpc[0]));
+  c->grid_short = grid(c->bpc[1]);
+  c->grid_win = grid(c->bpc[2]);
+  c->grid_body = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]);
+  c->kmode = t->path;
+  c->tstep = t->tstep == 1 ? 1 : 8;
+  c->dyn = t->static_tiles == 0;
+  c->tail_tile = std::min<uint32_t>(64, std::max<uint32_t>(8, (t->tail_tile ? t->tail_tile : 32) / 8 * 8));
+  c->tail_per_wave = t->tail_per_wave ? t->tail_per_wave : 1;
+  c->body_tail = std::min<uint32_t>(64, std::max<uint32_t>(8, (t->body_tail ? t->body_tail : 16) / 8 * 8));
+  c->ngroups_max = std::min<uint32_t>(CLAIM_GROUPS, t->groups);  // 0: by frame size
+  c->gshift = t->gshift < 0 ? ~0u : (uint32_t)t->gshift;         // ~0: by frame size
+}
+
 }  // namespace
 
 extern "C" {
 
 int oo_gpu_rx_abi_version(void) { return OO_GPU_RX_ABI_VERSION; }
+
+int oo_gpu_rx_set_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
+  if (c == nullptr || (t != nullptr && (t->path > 3 || t->grid_pct > 100))) return -EINVAL;
+  apply_tuning(c, t);
+  return 0;
+}
 
 int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   if (out == nullptr || cfg == nullptr) return -EINVAL;
@@ -775,29 +802,13 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) {
-    // Persistent grid: every resident block (occupancy query), optionally
-    // scaled by OO_RX_GRID_PCT for tuning.
-    const uint32_t pct = env_u32("OO_RX_GRID_PCT", 100);
-    const int b0 = oo_rx_blocks_per_cu();
-    if (b0 > 0)
-      c->grid = std::max<uint32_t>(1, (uint32_t)(b0 * prop.multiProcessorCount) * pct / 100);
-    const int b1 = oo_rx_blocks_per_cu_short();
-    if (b1 > 0)
-      c->grid_short = std::max<uint32_t>(1, (uint32_t)(b1 * prop.multiProcessorCount) * pct / 100);
-    const int bw = oo_rx_win_blocks_per_cu();
-    if (bw > 0) c->grid_win = (uint32_t)(bw * prop.multiProcessorCount);
-    const uint32_t bb = std::min<uint32_t>((uint32_t)std::max(0, oo_rx_body_blocks_per_cu()),
-                                           env_u32("OO_RX_BODY_BPC", 64));
-    if (bb > 0) c->grid_body = bb * (uint32_t)prop.multiProcessorCount;
+    // Persistent grids: every resident block (occupancy query).
+    c->ncu = (uint32_t)prop.multiProcessorCount;
+    const int b[4] = {oo_rx_blocks_per_cu(), oo_rx_blocks_per_cu_short(), oo_rx_win_blocks_per_cu(),
+                      oo_rx_body_blocks_per_cu()};
+    for (int k = 0; k < 4; ++k) c->bpc[k] = (uint32_t)std::max(0, b[k]);
   }
-  c->tstep = env_u32("OO_RX_TSTEP", 8) == 1 ? 1 : 8;
-  c->dyn = env_u32("OO_RX_STATIC", 0) == 0;
-  c->tail_tile = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_TAIL_TILE", 32) / 8 * 8));
-  c->tail_per_wave = env_u32("OO_RX_TAIL_PER_WAVE", 1);
-  c->body_tail = std::min<uint32_t>(64, std::max<uint32_t>(8, env_u32("OO_RX_BODY_TAIL", 16) / 8 * 8));
-  c->kmode = env_u32("OO_RX_KERNEL", 0);
-  c->ngroups_max = std::min<uint32_t>(CLAIM_GROUPS, env_u32("OO_RX_GROUPS", 0));  // 0: by frame size
-  c->gshift = env_u32("OO_RX_GSHIFT", ~0u);                                       // ~0: by frame size
+  apply_tuning(c, nullptr);
   DevTables& T = c->T;
   T.ip4_mask = c->ip4_mask;
   T.ip6_mask = c->ip6_mask;
@@ -1174,7 +1185,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   uint32_t* const sets = c->d_claim + 2u * 32u * oo_rx::CLAIM_LINES * track_index(c, trk);
   P.claim = sets + 32u * oo_rx::CLAIM_LINES * trk->parity;
   P.claim_next = sets + 32u * oo_rx::CLAIM_LINES * (trk->parity ^ 1u);
-  if (!tx && c->kmode == 0 && c->grid_win > 0 && c->grid_body > 0) {
+  if (!tx && (c->kmode == 0 || c->kmode == 3) && c->grid_win > 0 && c->grid_body > 0) {
     const int rc = launch_split(c, P, n, trk, P.claim, s);
     if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
     trk->parity ^= 1u;

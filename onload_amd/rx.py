@@ -78,6 +78,15 @@ class GpuRxStack:
         self.max_socks = max_socks
         self.host_stage_bytes = host_stage_bytes
         self.host_stage_pkts = host_stage_pkts
+        t = _abi.tuning_from_env() if device >= 0 else None
+        if t is not None:  # measurement settings of the Python process (tests, tools)
+            self.set_tuning(t)
+
+    def set_tuning(self, t: "_abi.Tuning | None") -> None:
+        """oo_gpu_rx_set_tuning: launch settings (None: the defaults)."""
+        rc = self._lib.oo_gpu_rx_set_tuning(self._ctx, ctypes.byref(t) if t is not None else None)
+        if rc != 0:
+            raise OSError(-rc, "oo_gpu_rx_set_tuning")
 
     @classmethod
     def wrap(cls, ctx, device: int, max_socks: int, lib) -> "GpuRxStack":
