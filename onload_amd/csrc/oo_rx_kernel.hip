@@ -187,6 +187,9 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
   return s;
 }
 
+#if defined(OO_RX_STAMPS) && !defined(OO_RX_EXPERIMENTS)
+#error "OO_RX_STAMPS is a diagnostic build (tools/build_ref.sh sets OO_RX_EXPERIMENTS)"
+#endif
 #ifdef OO_RX_STAMPS
 // Diagnostic phase stamps: stamps[((wave * 128 + iter) * 16) + phase] = realtime
 // (100 MHz) for the first 128 tiles of each wave.
@@ -1556,11 +1559,7 @@ __device__ __forceinline__ void issue_slot(IssueCursor& c, const Jobs& J, uint32
 __device__ __forceinline__ void issue_round(IssueCursor& c, const Jobs& J, uint64_t zero,
                                             void* slot, uint32_t lane) {
   glds<OO_RX_BODY_AUX>(c.a, slot);
-#ifdef OO_RX_ABL_LEAN
-  c.a += 128u;
-#else
   c.a += c.rnd < c.adv ? 128u : 0u;
-#endif
   if (++c.rnd == c.R) issue_slot(c, J, c.js + 1, lane, zero);
 }
 
@@ -1600,14 +1599,9 @@ __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, u
 // their words by 0).
 __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
                                               uint32_t lane) {
-#ifdef OO_RX_ABL_LEAN
-  const bool live = true, part = false;
-  if (true) {
-#else
   const bool live = c.rnd < c.lv;
   const bool part = live && c.rnd + 1u == c.lv && c.vb != 16u;
   if (__ballot(part) == 0) {
-#endif
     const uint32_t w = live ? 0x00010001u : 0u;
     uint32_t a = dot(v.x, w, c.acc);
     uint32_t b = dot(v.y, w, 0u);
@@ -1959,7 +1953,7 @@ __device__ __forceinline__ void gstore2(uint64_t a, uint32_t v) {
   *reinterpret_cast<g_uint16*>(a) = (uint16_t)v;
 }
 constexpr int NST_TX = 6;
-#if !defined(OO_RX_ABL_RX_ONLY) && !defined(OO_RX_SHORT)  // (timing builds: rx_kernel alone)
+#if !defined(OO_RX_SHORT)
 static_assert(R >= 4, "store_checks stages 64 lanes x 64 B in the ring");
 #endif
 __device__ __forceinline__ void store_checks(const KParams& P, const DescView& dv,
@@ -1967,13 +1961,8 @@ __device__ __forceinline__ void store_checks(const KParams& P, const DescView& d
                                              uint4 (*ring)[64]) {
   uint8_t* const frame = reinterpret_cast<uint8_t*>(dv.abase + (uint64_t)dv.shift);
   uint8_t* const sink = P.sink + 4u * lane;
-#ifdef OO_RX_ABL_TXSINK  // ablation builds only: every check to the sink
-  const bool whole = false, ip = false, l4 = false;
-  (void)frame;
-#else
   const bool whole = dv.valid && h.whole;
   const bool ip = dv.valid && !h.whole && h.ip_do, l4 = dv.valid && !h.whole && h.l4_do;
-#endif
   {
     uint4 hd[4] = {h.head[0], h.head[1], h.head[2], h.head[3]};
     hd[1].z = (hd[1].z & 0xffff0000u) | h.ip_ck;
@@ -2024,16 +2013,8 @@ __device__ __forceinline__ void store_checks(const KParams& P, const DescView& d
 // zeroing the set of the next one as it starts, so a wave ends with its last
 // record stores: nothing waits for the group's other claims.
 
-#ifdef OO_RX_ABL_NOHDR
-constexpr int NHS = 2;
-#else
 constexpr int NHS = HC + 2;
-#endif
-#ifdef OO_RX_ABL_NOSTORE
-constexpr int NST = 0;
-#else
 constexpr int NST = 2;
-#endif
 // Extra body rounds a long tile puts in flight in the header rows once the
 // parse has read them (the header work then overlaps E more KiB of stream).
 #ifndef OO_RX_EXTRA
@@ -2108,11 +2089,7 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
       const uint32_t a = lane_get(w[d], q), b = lane_get(w[4 + d], q);
       vw[d] = hi ? b : a;
     }
-#ifdef OO_RX_ABL_HOTSTORE  // ablation builds only: every tile's records to one of 32 hot 2-KiB runs
-    out[(size_t)((t.key & 31u) * 64u + q) * 2u + hi] = v;
-#else
     out[(size_t)(t.first + q) * 2u + hi] = v;
-#endif
   }
 }
 
@@ -2186,11 +2163,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   {
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
-#ifndef OO_RX_ABL_NOHDR  // ablation builds (timing experiments only; results are wrong)
     stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
-#else
-    (void)d0;
-#endif
   }
 
   uint32_t b = 0, it_ = 0;
@@ -2210,9 +2183,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     uint32_t myslot;
     const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot);
     uint32_t T0 = J.T;
-#ifdef OO_RX_ABL_NOBODY
-    T0 = 0;
-#endif
     bool ext = E > 0 && T0 > (uint32_t)(R + E);
     uint32_t T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
     if (lane == 0) lds_write4(&L.T0, T0);
@@ -2249,11 +2219,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       th = tx_header(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
       issue_extra();
     } else {
-#ifdef OO_RX_ABL_NOPARSE
-      ps = Parsed{};
-      ps.r.reason = (uint8_t)(lds_read16(&L.hdr[0][lane]).x & 7u);
-      issue_extra();
-#else
       const Hdr h = parse_headers(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
       issue_extra();
       STAMP(2, __builtin_amdgcn_s_memrealtime());
@@ -2263,7 +2228,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
                     true);
 #endif
       ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
-#endif
     }
     STAMP(3, __builtin_amdgcn_s_memrealtime());
 
@@ -2291,11 +2255,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     auto stage_next = [&]() {
       const Unit nt = unit_of(P, tnext);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
-#ifndef OO_RX_ABL_NOHDR
       stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
-#else
-      (void)dn;
-#endif
     };
     if (!ext) stage_next();
 
@@ -2372,18 +2332,12 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 
     const uint32_t body = lane_get(cc.bs, myslot);
     if constexpr (TX) {
-#ifndef OO_RX_ABL_RX_ONLY
       store_checks(P, dv, th, tx_l4_check(th, dv.shift, body), lane, L.ring);
-#else
-      (void)th;
-#endif
     } else {
       finish(ps, body);
       if (P.counters != nullptr && dv.valid)
         lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
-#ifndef OO_RX_ABL_NOSTORE
       store_records(P, tile, ps.r, lane);
-#endif
     }
     STAMP(5, __builtin_amdgcn_s_memrealtime());
     tcur = tnext;

@@ -2,7 +2,7 @@
 """Per-wave phase timeline of one rx_kernel launch (diagnostic).
 
 Needs a library built with -DOO_RX_STAMPS (``make variants
-VARIANTS="st:-DOO_RX_STAMPS"``), selected with OO_RX_LIB.  Prints where a
+VARIANTS="st:-DOO_RX_EXPERIMENTS,-DOO_RX_STAMPS"``), selected with OO_RX_LIB.  Prints where a
 wave's time goes per tile (header wait, parse, body stream, record) and how
 the waves' finish times spread.
 
