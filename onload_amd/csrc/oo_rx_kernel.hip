@@ -2406,14 +2406,27 @@ constexpr int WAVES_W = 2;  // win_kernel: waves per block
 #define OO_RX_WIN_WPE 4  // win_kernel: waves per SIMD the register budget allows
 #endif
 
+// 10 KiB a wave: sixteen waves fill a CU's 160 KiB (the per-reason counts
+// and the claim group stay in registers, reason_hist).
 struct WinLds {
   uint4 hdr[HC][64];             // header windows (stage_window)
   uint4 desc[2][64];             // descriptors of tile t (buffer t & 1) and t + 1
-  uint32_t cnt[OO_RX_R_COUNT];   // per-reason counts
-  uint32_t dbase, gofs, pad0, pad1;
 };
-static_assert(sizeof(WinLds) % 16 == 0, "WinLds is carved from a uint4 array");
+static_assert(sizeof(WinLds) == 10240, "sixteen waves per CU");
 constexpr int WIN_U4 = (int)(sizeof(WinLds) / 16);
+
+// Lane k < 32: how many lanes of `valid` have reason k (five ballots of the
+// reason's bits; the lane's own bits select each ballot or its complement).
+__device__ __forceinline__ uint32_t reason_hist(uint32_t reason, bool valid, uint32_t lane) {
+  static_assert(OO_RX_R_COUNT == 32, "five reason bits");
+  uint64_t m = __ballot(valid);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const uint64_t bj = __ballot((reason >> j) & 1u);
+    m &= ((lane >> j) & 1u) ? bj : ~bj;
+  }
+  return (uint32_t)__popcll(m);
+}
 
 // win_kernel's tile loop.  The same tiles, descriptor and window staging,
 // parse, demux and claims as tile_loop, without a body: while tile t's
@@ -2435,13 +2448,9 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
   const uint32_t W = gridDim.x * WAVES_W;
   if (gwave == 0) zero_claim_set(P.claim_next, lane);
   uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
-  if (lane == 0) {
-    const uint32_t g = group_of(P, gwave);
-    lds_write4(&L.dbase, 3u * W + g);
-    lds_write4(&L.gofs, 32u * g);
-  }
+  const uint32_t g = sreg(group_of(P, gwave));
   if (gwave >= P.ntiles) return;
-  if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
+  uint32_t cnt = 0;  // lane k < 32: this wave's count of reason k
 
   // Prologue: tile t0's descriptors and windows, then t1's descriptors.
   {
@@ -2462,14 +2471,18 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     if (it_ == 0) vm_wait<1>();
     else vm_wait<2 + NST>();
     const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), tile, lane);
-    const Hdr h = parse_headers(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
+    // (the window's cell addresses recomputed per tile: hoisted, eight
+    // loop-long registers would spill)
+    uint32_t wl = lane;
+    asm volatile("" : "+v"(wl));
+    const Hdr h = parse_headers(window_of(L.hdr, wl), dv.shift, dv.len, dv.abase);
 
     // ---- stage the next tile: its windows into the rows the parse has
     // read (its descriptor line: newer are the claim and the record stores),
     // the descriptors of the tile after it, the claim of the tile after that.
     if (it_ != 0) {
       const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
-      tnext2 = P.dyn ? sreg(lds_read4(&L.dbase)) + c : tnext2 + W;
+      tnext2 = P.dyn ? 3u * W + g + c : tnext2 + W;
       vm_wait<1 + NST>();
     } else {
       vm_wait<0>();
@@ -2481,11 +2494,11 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
     }
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
-    claim_tile(P.claim + sreg(lds_read4(&L.gofs)), P.ngroups, lane, got);
+    claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
 
     // ---- lookups and the record.
     Parsed ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
-    if (P.counters != nullptr && dv.valid) lds_add4(&L.cnt[ps.r.reason & (OO_RX_R_COUNT - 1)], 1u);
+    const uint32_t reason = ps.r.reason;
     store_records(P, tile, ps.r, lane);
     // The pending words of a tile holding frames with a body.
     const bool body = dv.span > HB;
@@ -2500,17 +2513,11 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       if (__ballot(wait) != 0 && lane == 0)
         __hip_atomic_store(P.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (P.counters != nullptr) cnt += reason_hist(reason, dv.valid, lane);
     tcur = tnext;
     tnext = tnext2;
   }
-  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  if (P.counters != nullptr) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (ln < OO_RX_R_COUNT) {
-      const uint32_t c = lds_read4(&L.cnt[ln]);
-      if (c != 0) atomicAdd(&P.counters[ln], c);
-    }
-  }
+  if (P.counters != nullptr && lane < OO_RX_R_COUNT && cnt != 0) atomicAdd(&P.counters[lane], cnt);
 }
 
 __global__ __launch_bounds__(WAVES_W * 64) __attribute__((amdgpu_waves_per_eu(OO_RX_WIN_WPE))) void win_kernel(

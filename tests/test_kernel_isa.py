@@ -104,3 +104,40 @@ def test_short_kernel_same_invariants(asm_short):
     assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
     assert len(re.findall(r"global_store_dword\b", rx)) == 3  # zero_claim_set
     assert not re.findall(r"flat_store|flat_load|flat_atomic", rx)
+
+
+WIN = "_ZN5oo_rx10win_kernelENS_7KParamsE"
+BODY = "_ZN5oo_rx11body_kernelENS_7KParamsE"
+
+
+def _lds(stderr, mangled):
+    i = stderr.index(f"Function Name: {mangled}")
+    return int(re.search(r"LDS Size \[bytes/block\]: (\d+)", stderr[i:i + 2000]).group(1))
+
+
+def test_split_kernels_no_scratch(asm):
+    """The split transform (win_kernel, body_kernel): no spill -- a reload in
+    the tile loop would wait for the staged next tile's windows -- and
+    win_kernel fits sixteen waves per CU (128 VGPRs, 10 KiB LDS a wave)."""
+    text, stderr = asm
+    for k in (WIN, BODY):
+        u = _usage(stderr, k)
+        assert u["VGPRs Spill"] == 0, (k, u)
+        assert "scratch_" not in _body(text, k), k
+    assert _usage(stderr, WIN)["VGPRs"] <= 128
+    assert _lds(stderr, WIN) <= 2 * 10240
+    assert _usage(stderr, BODY)["VGPRs"] <= 128
+
+
+def test_split_store_counts(asm):
+    text, _ = asm
+    w = _body(text, WIN)
+    # store_records (NST = 2), the pending word, and the sc1 stores: three in
+    # zero_claim_set plus the body flag
+    assert len(re.findall(r"global_store_dwordx4", w)) == 2
+    assert len(re.findall(r"global_store_dwordx2", w)) == 1
+    assert len(re.findall(r"global_store_dword .* sc1$", w, re.M)) == 4
+    assert len(re.findall(r"global_store_dword\b", w)) == 4
+    assert not re.findall(r"global_store_(byte|short)", w)
+    for k in (WIN, BODY):
+        assert not re.findall(r"flat_store|flat_load|flat_atomic", _body(text, k)), k
