@@ -461,7 +461,8 @@ int oo_gpu_rx_group_sock_set(oo_gpu_rx_group* g, int32_t sock_id, const oo_gpu_r
 int oo_gpu_rx_group_split(const oo_gpu_rx_group* g, const oo_gpu_pkt_desc* desc, uint32_t n,
                           uint32_t parts, uint32_t* first);
 /* In one process: member i transforms shards[i], asynchronously on its
- * stream (oo_gpu_rx_process_dev). */
+ * stream (oo_gpu_rx_process_dev): work the caller queued on other streams
+ * (the fill of a shard's buffers) must be ordered before it by the caller. */
 int oo_gpu_rx_group_process(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards);
 /* In one process, after process: the members' records into dst (sum of
  * the shards' n, member order; device or host memory, NULL: none), each

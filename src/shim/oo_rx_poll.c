@@ -425,16 +425,24 @@ static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs
 }
 
 /* Step 3: wait for the chunk's batch, then dispatch every event in order.
- * The chunk's counters are added to *st only if its batch ran. */
+ * The chunk's counters are added to *st only if its batch ran.  A callback
+ * that changes the tables (a filter inserted on an accept, removed on a
+ * close, next to ci_netif_filter_insert / _remove) while transformed events
+ * of the chunk are still to come: the reference loop, one event after
+ * another, runs those on the new tables, so they are transformed again
+ * (counted in n_resubmit; their first records are discarded, nothing was
+ * dispatched from them). */
 static int chunk_complete(oo_rx_poll* p, struct chunk* c, oo_rx_poll_stats* st)
 {
   uint32_t i, m = 0;
+  uint64_t gen;
   if( c->busy ) {
     int rc = oo_gpu_rx_wait(p->gpu, c->ticket);
     c->busy = 0;
     if( rc < 0 )
       return rc;
   }
+  gen = oo_gpu_rx_table_gen(p->gpu);
   for( i = 0; i < c->n; ++i ) {
     const oo_rx_poll_ev* e = &c->evs[i];
     if( c->what[i] == W_OTHER ) {
@@ -460,6 +468,30 @@ static int chunk_complete(oo_rx_poll* p, struct chunk* c, oo_rx_poll_stats* st)
         }
         dispatch(p, e->rq_id, frame, r, &c->st);
       }
+    }
+    if( m < c->m && oo_gpu_rx_table_gen(p->gpu) != gen ) {
+      /* The rest of the chunk becomes a chunk of its own, transformed on the
+       * new tables.  Its events were classified (and counted) already: only
+       * the batch or the hand-back is added to the counters. */
+      const oo_rx_poll_stats saved = c->st;
+      uint64_t handed;
+      int rc = chunk_submit(p, c, c->evs + i + 1, c->n - i - 1, &saved);
+      handed = c->st.n_handback - saved.n_handback;
+      c->st = saved;
+      c->st.n_handback += handed;
+      ++c->st.n_resubmit;
+      if( rc < 0 )
+        return rc;
+      if( c->busy ) {
+        ++c->st.n_batches;
+        rc = oo_gpu_rx_wait(p->gpu, c->ticket);
+        c->busy = 0;
+        if( rc < 0 )
+          return rc;
+      }
+      gen = oo_gpu_rx_table_gen(p->gpu);
+      i = (uint32_t)-1;  /* from the rest's first event */
+      m = 0;
     }
   }
   *st = c->st;
@@ -497,6 +529,7 @@ int oo_rx_poll_evs(oo_rx_poll* p, const oo_rx_poll_ev* evs, uint32_t n,
       k = n - issued < p->cfg.evs_per_poll ? n - issued : p->cfg.evs_per_poll;
       sub_rc = chunk_submit(p, nx, evs + issued, k, &base);
     }
+    const uint32_t cn = c->n;  /* (a re-transformed rest replaces c's events) */
     gen = oo_gpu_rx_table_gen(p->gpu);
     rc = chunk_complete(p, c, stats);
     if( rc == 0 && more && sub_rc == 0 && oo_gpu_rx_table_gen(p->gpu) != gen ) {
@@ -521,7 +554,7 @@ int oo_rx_poll_evs(oo_rx_poll* p, const oo_rx_poll_ev* evs, uint32_t n,
       }
       return done > 0 ? (int)done : rc;
     }
-    done += c->n;
+    done += cn;
     if( !more )
       return (int)done;
     if( sub_rc < 0 )

@@ -40,8 +40,11 @@ def test_group_of_three_on_one_gpu_matches_unsharded_oracle(cuda, config, n):
         shards.append(Shard(frames.data_ptr(), frames.numel(), d_desc.data_ptr() + 16 * f, c, 0,
                             outs[-1].data_ptr(), ctrs[-1].data_ptr(),
                             streams[-1].cuda_stream))
-    g.process(shards)
     dst = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    # the buffers were filled on torch's stream; the shards' streams are not
+    # ordered after it (as with any caller's streams)
+    torch.cuda.synchronize()
+    g.process(shards)
     counters = np.zeros(32, dtype=np.uint32)
     g.gather(shards, dst.data_ptr(), counters)
     got = dst.cpu().numpy().view(_abi.RESULT_DTYPE)

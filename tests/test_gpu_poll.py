@@ -178,10 +178,10 @@ def test_poll_counters_match_reference_run(cuda, name):
 @pytest.mark.parametrize("evs_per_poll", (16, 64))
 def test_poll_table_change_in_a_callback(cuda, evs_per_poll):
     """A callback that changes the tables (a filter removed as its socket
-    closes, next to ci_netif_filter_remove) while the next chunk is already
-    transformed: the packets after it see the new tables, as the reference's
-    one-event-at-a-time loop would -- the shim transforms that
-    chunk again."""
+    closes, next to ci_netif_filter_remove) while the rest of its chunk and
+    the next chunk are already transformed: the packets after it see the new
+    tables, as the reference's one-event-at-a-time loop would --
+    the shim transforms both again."""
     import cases
     socks, filters = cases.order_world()
     g = GpuRxStack(device=0, host_stage_bytes=16 << 20, host_stage_pkts=4096)
@@ -211,6 +211,7 @@ def test_poll_table_change_in_a_callback(cuda, evs_per_poll):
     assert p.poll(evs) == n
     stages = [int(r["stage"]) for r in rec.recs]
     assert stages == [1] * (cut + 1) + [2] * (n - cut - 1)
-    assert p.stats.n_resubmit == 1
+    assert p.stats.n_resubmit == 2  # the chunk's rest, then the next chunk
+    assert p.stats.n_batches == n // evs_per_poll + 2
     p.close()
     g.close()
