@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread \
     ${TESTS_K:-} > gpurun_out/gpu_tests.log 2>&1
   rc=$?
   tail -5 gpurun_out/gpu_tests.log
