@@ -2436,9 +2436,8 @@ __device__ __forceinline__ uint32_t reason_hist(uint32_t reason, bool valid, uin
 // tile's start).  Counted waits, as tile_loop ("rx_kernel" above): per tile
 // HC window rows, one descriptor line and the claim, then the demux loads
 // (each level ends in vmcnt(0)), then NST record stores, and -- only for
-// tiles holding a frame with a body -- the pending words and the body flag
-// (uncounted: an operation the count leaves out only makes a wait
-// stricter).
+// tiles holding a frame with a body -- the pending words (uncounted: an
+// operation the count leaves out only makes a wait stricter).
 __device__ __forceinline__ void window_loop(const KParams& P) {
   __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_W * WIN_U4];
   const int wave = (int)(threadIdx.x >> 6);
@@ -2450,7 +2449,8 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
   uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
   const uint32_t g = sreg(group_of(P, gwave));
   if (gwave >= P.ntiles) return;
-  uint32_t cnt = 0;  // lane k < 32: this wave's count of reason k
+  uint32_t cnt = 0;    // lane k < 32: this wave's count of reason k
+  bool waits = false;  // a frame of this wave's tiles waits for its body
 
   // Prologue: tile t0's descriptors and windows, then t1's descriptors.
   {
@@ -2510,14 +2510,17 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
                           ((uint32_t)ps.r.reason << 24);
       const uint32_t hi = (uint32_t)ps.r.vlan | ((uint32_t)ps.r.ip_paylen << 16);
       if (lane < tile.cnt) P.pend[tile.first + lane] = (uint64_t)lo | ((uint64_t)hi << 32);
-      if (__ballot(wait) != 0 && lane == 0)
-        __hip_atomic_store(P.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      waits = waits || __ballot(wait) != 0;
     }
     if (P.counters != nullptr) cnt += reason_hist(reason, dv.valid, lane);
     tcur = tnext;
     tnext = tnext2;
   }
   if (P.counters != nullptr && lane < OO_RX_R_COUNT && cnt != 0) atomicAdd(&P.counters[lane], cnt);
+  // The body flag, once a wave and after its tiles: every wave storing to
+  // the one line per tile serializes the stores, and the tile loop's counted
+  // waits would wait for them.
+  if (waits && lane == 0) __hip_atomic_store(P.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(WAVES_W * 64) __attribute__((amdgpu_waves_per_eu(OO_RX_WIN_WPE))) void win_kernel(
