@@ -20,7 +20,8 @@ HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 # static vmcnt waits are written in terms of these constants;
 # tests/test_gpu_wait_variants.py runs parity on every build.
 CHECK_VARIANTS := r6e4:-DOO_RX_RING=6,-DOO_RX_EXTRA=4 r8e2:-DOO_RX_RING=8,-DOO_RX_EXTRA=2 \
-                  w1e0:-DOO_RX_WAVES=1,-DOO_RX_EXTRA=0
+                  w1e0:-DOO_RX_WAVES=1,-DOO_RX_EXTRA=0 rb6:-DOO_RX_BODY_RING=6 \
+                  rb12:-DOO_RX_BODY_RING=12,-DOO_RX_WIN_WPE=3
 CHECKS := $(foreach v,$(CHECK_VARIANTS),build/check/liboo_gpu_rx_$(firstword $(subst :, ,$(v))).so)
 
 all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling tools/ring_probe tools/poll_bench $(CHECKS)

@@ -1185,7 +1185,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   uint32_t* const sets = c->d_claim + 2u * 32u * oo_rx::CLAIM_LINES * track_index(c, trk);
   P.claim = sets + 32u * oo_rx::CLAIM_LINES * trk->parity;
   P.claim_next = sets + 32u * oo_rx::CLAIM_LINES * (trk->parity ^ 1u);
-  if (!tx && (c->kmode == 0 || c->kmode == 3) && c->grid_win > 0 && c->grid_body > 0) {
+  if (!tx && c->kmode == 3 && c->grid_win > 0 && c->grid_body > 0) {
     const int rc = launch_split(c, P, n, trk, P.claim, s);
     if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
     trk->parity ^= 1u;

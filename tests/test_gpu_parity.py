@@ -207,7 +207,9 @@ def test_full_size_config5_last_shard_bit_exact(cuda):
                                  {"OO_RX_GSHIFT": "4", "OO_RX_GROUPS": "8"}, {"OO_RX_GSHIFT": "4"},
                                  {"OO_RX_GSHIFT": "5", "OO_RX_GROUPS": "16", "OO_RX_GRID_PCT": "37"},
                                  {"OO_RX_GSHIFT": "0", "OO_RX_GROUPS": "64"}, {"OO_RX_KERNEL": "1"},
-                                 {"OO_RX_KERNEL": "2", "OO_RX_GRID_PCT": "37"}])
+                                 {"OO_RX_KERNEL": "2", "OO_RX_GRID_PCT": "37"},
+                                 {"OO_RX_KERNEL": "3"}, {"OO_RX_KERNEL": "3", "OO_RX_BODY_TAIL": "64"},
+                                 {"OO_RX_KERNEL": "3", "OO_RX_GRID_PCT": "37", "OO_RX_BODY_BPC": "2"}])
 def test_tile_partitions_and_claim_reuse(cuda, env, monkeypatch):
     """Static and dynamic (claimed) tile schedules with several tail shapes
     give the same records; 40 launches in a row reuse every claim-counter
@@ -230,11 +232,12 @@ def test_tile_partitions_and_claim_reuse(cuda, env, monkeypatch):
     g.close()
 
 
-@pytest.mark.parametrize("kernel", ["1", "2"])
+@pytest.mark.parametrize("kernel", ["1", "2", "3"])
 def test_both_rx_kernels_on_every_corpus(cuda, kernel, monkeypatch):
     """The 4-slot-ring rx_kernel (long frames) and the 2-slot one (short
     frames, 12 waves per CU) are chosen per launch by buffer bytes per packet
-    (oo_gpu_rx.cpp launch()); forced here (OO_RX_KERNEL 1 / 2), each must be
+    (oo_gpu_rx.cpp launch()); forced here (OO_RX_KERNEL 1 / 2, and 3: the
+    split transform, win_kernel + body_kernel), each must be
     bit-exact on the edge corpus at odd and even alignments and on samples of
     every configuration, with several launches per context."""
     monkeypatch.setenv("OO_RX_KERNEL", kernel)

@@ -9,7 +9,9 @@ header-row rounds E, the staging operations per tile and the stores per tile
 block with E 0); each build is loaded beside the product (its own soname) and
 must stay bit-exact with the oracle -- a count that does not follow its
 constants shows up here as wrong sums, not only when the product's values
-change."""
+change.  The split transform's body ring (RB, oo_rx_kernel.hip body_loop)
+has its own builds (rb6, rb12 -- the latter with win_kernel at three waves
+per SIMD), run through the split path (OO_RX_KERNEL 3)."""
 import os
 
 import numpy as np
@@ -25,6 +27,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VARIANTS = ("r6e4", "r8e2", "w1e0")
+SPLIT_VARIANTS = ("rb6", "rb12")
 HWPORTS = (0, 1, 3, 2, 5)
 _libs: dict = {}
 
@@ -51,8 +54,10 @@ def _check(g, o, buf, desc):
     np.testing.assert_array_equal(ctr, counters_of(want))
 
 
-@pytest.mark.parametrize("variant", VARIANTS)
-def test_variant_edge_corpus(cuda, variant):
+@pytest.mark.parametrize("variant", VARIANTS + SPLIT_VARIANTS)
+def test_variant_edge_corpus(cuda, variant, monkeypatch):
+    if variant in SPLIT_VARIANTS:
+        monkeypatch.setenv("OO_RX_KERNEL", "3")
     g = GpuRxStack(device=0, intf_hwport=HWPORTS, lib=_lib(variant))
     o = OracleStack(intf_hwport=HWPORTS)
     install(g, edge_world())
@@ -62,9 +67,11 @@ def test_variant_edge_corpus(cuda, variant):
         _check(g, o, buf, desc)
 
 
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS + SPLIT_VARIANTS)
 @pytest.mark.parametrize("config,n", [(2, 1 << 14), (3, 1 << 16), (4, 1 << 13), (5, 1 << 15)])
-def test_variant_config_samples(cuda, variant, config, n):
+def test_variant_config_samples(cuda, variant, config, n, monkeypatch):
+    if variant in SPLIT_VARIANTS:
+        monkeypatch.setenv("OO_RX_KERNEL", "3")
     filters, socks = pktgen.world(config)
     g = GpuRxStack(device=0, lib=_lib(variant))
     o = OracleStack()

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 check on a GPU box: the -m gpu suite, then same-box bench lines of
-# the split transform (default) against the single-kernel instances
-# (OO_RX_KERNEL=1: 4-slot ring, =2: 2-slot ring) on configs 2-5.
+# the product's auto path against the split transform (OO_RX_KERNEL=3) on
+# configs 2-5 (LIBS: other builds or settings, path@VAR=val).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
@@ -13,5 +13,5 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   [ $rc -ne 0 ] && exit $rc
 fi
 REPS=${REPS:-1} CONFIGS="${CONFIGS:-2 3 4 5}" STEPS=${STEPS:-20} \
-  LIBS="${LIBS:-onload_amd/liboo_gpu_rx.so onload_amd/liboo_gpu_rx.so@OO_RX_KERNEL=1 onload_amd/liboo_gpu_rx.so@OO_RX_KERNEL=2}" \
+  LIBS="${LIBS:-onload_amd/liboo_gpu_rx.so onload_amd/liboo_gpu_rx.so@OO_RX_KERNEL=3}" \
   bash tools/ab.sh 2>&1 | tee gpurun_out/ab.log
