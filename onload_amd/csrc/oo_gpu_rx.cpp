@@ -1115,16 +1115,16 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   B.flag = A.flag = set + 32u * oo_rx::FLAG_LINE;
   // win_kernel: header-bound tiles, many claims per us (32 groups of
   // 16-wave runs, each over all eight XCDs).
-  const uint64_t WB = (uint64_t)c->grid_win * (uint32_t)oo_rx_win_waves_per_block();
+  const uint32_t wpb_w = (uint32_t)oo_rx_win_waves_per_block();
   const uint32_t blocks_b =
-      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + 1) / 2, c->grid_win));
-  const uint64_t WBl = (uint64_t)blocks_b * (uint32_t)oo_rx_win_waves_per_block();
-  (void)WB;
+      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + wpb_w - 1) / wpb_w, c->grid_win));
+  const uint64_t WBl = (uint64_t)blocks_b * wpb_w;
   set_groups(B, WBl, 32u, 4u);
   set_tiles_dyn(B, n, WBl, c->tail_tile, c->tail_per_wave);
   // body_kernel: stream-bound units (64 single-wave groups), a finer tail.
+  const uint32_t wpb_b = (uint32_t)oo_rx_body_waves_per_block();
   const uint32_t blocks_a =
-      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + 1) / 2, c->grid_body));
+      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + wpb_b - 1) / wpb_b, c->grid_body));
   const uint64_t WA = (uint64_t)blocks_a * (uint32_t)oo_rx_body_waves_per_block();
   A.claim = set + 32u * CLAIM_GROUPS;
   A.claim_next = nullptr;
@@ -1185,7 +1185,11 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   uint32_t* const sets = c->d_claim + 2u * 32u * oo_rx::CLAIM_LINES * track_index(c, trk);
   P.claim = sets + 32u * oo_rx::CLAIM_LINES * trk->parity;
   P.claim_next = sets + 32u * oo_rx::CLAIM_LINES * (trk->parity ^ 1u);
-  if (!tx && c->kmode == 3 && c->grid_win > 0 && c->grid_body > 0) {
+  // The split transform: win_kernel holds the occupancy bitmaps in LDS, so
+  // only for tables that fit there (oo_rx_kernel.hip OCC_LDS_MAX4 / _MAX6).
+  const bool split_fits = (uint64_t)c->ip4_mask + 1 <= oo_rx::OCC_LDS_MAX4 &&
+                          (uint64_t)c->ip6_mask + 1 <= oo_rx::OCC_LDS_MAX6;
+  if (!tx && c->kmode == 3 && split_fits && c->grid_win > 0 && c->grid_body > 0) {
     const int rc = launch_split(c, P, n, trk, P.claim, s);
     if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
     trk->parity ^= 1u;

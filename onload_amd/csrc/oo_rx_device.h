@@ -146,6 +146,15 @@ constexpr uint32_t CLAIM_GROUPS = 64;
 // One claim set: the window (or tile) kernel's group counters, the body
 // kernel's group counters, and the body flag, each on a 128-B line.
 constexpr uint32_t CLAIM_LINES = 2 * CLAIM_GROUPS + 1;
+
+// A win_kernel block's copy of the occupancy bitmaps: the IPv4 bitmap at 0,
+// the IPv6 one at OCC_LDS_B6, the intf -> hwport bytes at OCC_LDS_HW.  Tables
+// of up to 2^16 IPv4 / 2^14 IPv6 slots (the defaults) fit; larger ones take
+// the single-kernel path.
+constexpr uint32_t OCC_LDS_B6 = 8192;
+constexpr uint32_t OCC_LDS_HW = 8192 + 2048;
+constexpr uint32_t OCC_LDS_BYTES = OCC_LDS_HW + 32;
+constexpr uint32_t OCC_LDS_MAX4 = 1u << 16, OCC_LDS_MAX6 = 1u << 14;
 constexpr uint32_t FLAG_LINE = 2 * CLAIM_GROUPS;
 
 // The split transform's pending word of a frame with a body (KParams::pend,

@@ -47,6 +47,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "oo_rx_device.h"
 
 // OO_RX_SHORT (oo_rx_kernel_short.hip): the same rx_kernel with a 2-slot
@@ -282,6 +284,16 @@ struct Probe {
   uint64_t occ, slots;  // this lane's table (per tile: not loop-invariant)
   uint32_t mask;
   bool is6;
+  static constexpr bool kLds = false;
+};
+// The same with the occupancy bitmaps (and the intf -> hwport bytes) copied
+// into the block's LDS (win_kernel): `lo` is the LDS address of this lane's
+// family's bitmap.  The bit reads then leave the vector-memory path, whose
+// scattered 64-line requests saturate the CU's texture units on short
+// frames (TA / TD busy 78 / 95 %, config 3).
+struct ProbeL : Probe {
+  uint32_t lo;
+  static constexpr bool kLds = true;
 };
 
 // A kernel-argument value forced into a scalar register: a per-lane select
@@ -332,6 +344,33 @@ __device__ __forceinline__ Probe probe_of(const KParams& P, bool is6) {
 // address ha (netif_table.h:33, in HBM beside the zero region; a per-lane
 // index, so a vector load, which here costs no wait of its own -- inside the
 // walks its wait would drain the body stream).
+__device__ __forceinline__ void occ_words6(const ProbeL& t, const uint32_t i[6], uint32_t w[6],
+                                           uint64_t ha, uint32_t& hw) {
+  uint32_t a[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) a[k] = t.lo + 4u * (i[k] >> 5);
+  asm volatile(
+      "ds_read_b32 %0, %7\n\tds_read_b32 %1, %8\n\tds_read_b32 %2, %9\n\t"
+      "ds_read_b32 %3, %10\n\tds_read_b32 %4, %11\n\tds_read_b32 %5, %12\n\t"
+      "ds_read_u8 %6, %13\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(hw)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"((uint32_t)ha)
+      : "memory");
+}
+__device__ __forceinline__ void occ_words4(const ProbeL& t, const uint32_t i[4], uint32_t w[4],
+                                           uint64_t ha, uint32_t& hw) {
+  uint32_t a[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a[k] = t.lo + 4u * (i[k] >> 5);
+  asm volatile(
+      "ds_read_b32 %0, %5\n\tds_read_b32 %1, %6\n\tds_read_b32 %2, %7\n\t"
+      "ds_read_b32 %3, %8\n\tds_read_u8 %4, %9\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(hw)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"((uint32_t)ha)
+      : "memory");
+}
 __device__ __forceinline__ void occ_words6(const Probe& t, const uint32_t i[6], uint32_t w[6],
                                            uint64_t ha, uint32_t& hw) {
   uint64_t a[6];
@@ -367,8 +406,15 @@ __device__ __forceinline__ bool probe_occ(const KParams& P, const Probe& t, uint
   (void)P;
   return ((gload4(t.occ + 4u * (i >> 5)) >> (i & 31u)) & 1u) != 0;
 }
+__device__ __forceinline__ bool probe_occ(const KParams& P, const ProbeL& t, uint32_t i) {
+  (void)P;
+  uint32_t w;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(t.lo + 4u * (i >> 5)) : "memory");
+  return ((w >> (i & 31u)) & 1u) != 0;
+}
 
-__device__ __forceinline__ Rec load_rec(const KParams& P, const Probe& t, uint32_t i, bool any6) {
+template <class PR>
+__device__ __forceinline__ Rec load_rec(const KParams& P, const PR& t, uint32_t i, bool any6) {
   (void)P;
   const uint64_t a = t.slots + ((uint64_t)i << (t.is6 ? 6 : 5));
   Rec r;
@@ -433,8 +479,8 @@ __device__ __forceinline__ bool rec_match(const KParams& P, const Rec& r, bool f
 // One slot against the lookup key for a lane of either family: M = 0 IPv4,
 // 1 IPv6, 2 per lane (t.is6) -- both compares, no loads, so a wave holding
 // both families walks in one instruction stream.
-template <int M>
-__device__ __forceinline__ bool rec_match_m(const KParams& P, const Probe& t, const Rec& r,
+template <int M, class PR>
+__device__ __forceinline__ bool rec_match_m(const KParams& P, const PR& t, const Rec& r,
                                             bool first4, const uint32_t la[4], uint32_t lp,
                                             const uint32_t ra[4], bool ra_null, uint32_t rp,
                                             uint32_t proto, uint32_t hwp, int vlan, int32_t& id) {
@@ -459,8 +505,8 @@ __device__ __forceinline__ bool rec_match_m(const KParams& P, const Probe& t, co
 // walk there (handle_entry, netif_table.c:225-229); UDP counts every match
 // (ci_udp_rx_deliver continues past a multicast destination or a socket
 // that drops, udp_rx.c:194-228).
-template <int M>
-__device__ Match walk(const KParams& P, const Probe& t, bool any6, const uint32_t la[4],
+template <int M, class PR>
+__device__ Match walk(const KParams& P, const PR& t, bool any6, const uint32_t la[4],
                       uint32_t lp, const uint32_t ra[4], bool ra_null, uint32_t rp, uint32_t proto,
                       uint32_t hwp, int vlan, uint32_t h1, uint32_t h2, bool occ, Rec rec, bool have,
                       bool occ_next, bool stop) {
@@ -938,8 +984,8 @@ __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, u
 // first stage with a match decides (*stage = 1..3).  M as rec_match_m: a wave
 // holding both families walks them together (M = 2), so its walks cost the
 // dependent loads of one family, not of both in turn.
-template <int M, bool PRE1>
-__device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t, bool any6,
+template <int M, bool PRE1, class PR>
+__device__ __forceinline__ Match lookup_stages(const KParams& P, const PR& t, bool any6,
                                                const Hdr& h, uint32_t dport, uint32_t sport,
                                                uint32_t proto, uint32_t hwp, int vlan, bool tcp,
                                                uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
@@ -997,8 +1043,8 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const Probe& t,
 #ifndef OO_RX_FSM
 #define OO_RX_FSM 1
 #endif
-template <int M>
-__device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bool any6,
+template <int M, class PR>
+__device__ __forceinline__ Match lookup_fsm(const KParams& P, const PR& t, bool any6,
                                             const Hdr& h, uint32_t dport, uint32_t sport,
                                             uint32_t proto, uint32_t hwp, int vlan, bool tcp,
                                             uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
@@ -1100,9 +1146,12 @@ __device__ __forceinline__ Match lookup_fsm(const KParams& P, const Probe& t, bo
 // every stage's first-slot and next-slot occupancy bits are loaded together,
 // then the first slots' records, so a wave pays two dependent loads however
 // its packets mix address families and protocols.
-template <bool ANY6>
+// LO: the occupancy bitmaps and the hwport bytes are in LDS at lds_occ
+// (OccLds layout, win_kernel).
+template <bool ANY6, bool LO>
 __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h, int intf_i,
-                                                 uint64_t abase, int span, int shift) {
+                                                 uint64_t abase, int span, int shift,
+                                                 uint32_t lds_occ) {
   const int vlan = (int)h.vlan;
   const uint32_t proto = h.proto;
   uint32_t reason = h.reason;
@@ -1121,11 +1170,19 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
   bool s2 = false;
   if (__ballot(look) != 0) {
     constexpr bool any6 = ANY6;
-    const Probe t = probe_of(P, ANY6 && is6);
+    typedef typename std::conditional<LO, ProbeL, Probe>::type PR;
+    PR t;
+    static_cast<Probe&>(t) = probe_of(P, ANY6 && is6);
     // (intf_i_to_hwport for a valid interface; lanes with none read entry 0
     // and take 0xff)
     const bool intf_ok = (uint32_t)intf_i < (uint32_t)OO_GPU_RX_MAX_INTF;
-    const uint64_t hwa = sreg64(P.hwport) + (intf_ok ? (uint32_t)intf_i : 0u);
+    uint64_t hwa;
+    if constexpr (LO) {
+      t.lo = lds_occ + (ANY6 && is6 ? OCC_LDS_B6 : 0u);
+      hwa = lds_occ + OCC_LDS_HW + (intf_ok ? (uint32_t)intf_i : 0u);
+    } else {
+      hwa = sreg64(P.hwport) + (intf_ok ? (uint32_t)intf_i : 0u);
+    }
     uint32_t hwp = 0xffu;
     const bool tcp = proto == 6u;
     const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & t.mask;
@@ -1238,11 +1295,13 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
 
 // A wave whose lookups are all IPv4 takes the IPv4-only instance (the
 // IPv6 compares and record halves compiled out).
+template <bool LO = false>
 __device__ __forceinline__ Parsed demux_packet(const KParams& P, const Hdr& h, int intf_i,
-                                               uint64_t abase, int span, int shift) {
+                                               uint64_t abase, int span, int shift,
+                                               uint32_t lds_occ = 0) {
   if (__ballot(h.is6 && h.reason == PENDING && h.late == PENDING) != 0)
-    return demux_packet_t<true>(P, h, intf_i, abase, span, shift);
-  return demux_packet_t<false>(P, h, intf_i, abase, span, shift);
+    return demux_packet_t<true, LO>(P, h, intf_i, abase, span, shift, lds_occ);
+  return demux_packet_t<false, LO>(P, h, intf_i, abase, span, shift, lds_occ);
 }
 
 // The verdict a long packet's record waited for: the window part plus the
@@ -2401,19 +2460,21 @@ __device__ __forceinline__ uint32_t body_target(uint32_t s4, uint32_t pseudo, bo
   return (2u * 0xffffu - r4 - rp) % 0xffffu;
 }
 
-constexpr int WAVES_W = 2;  // win_kernel: waves per block
+constexpr int WAVES_W = 4;  // win_kernel: waves per block (sharing one bitmap copy)
 #ifndef OO_RX_WIN_WPE
 #define OO_RX_WIN_WPE 4  // win_kernel: waves per SIMD the register budget allows
 #endif
 
-// 10 KiB a wave: sixteen waves fill a CU's 160 KiB (the per-reason counts
-// and the claim group stay in registers, reason_hist).
+// 10 KiB a wave (the per-reason counts and the claim group stay in
+// registers, reason_hist), plus the block's bitmap copy: 50 KiB a block, three
+// blocks (12 waves) per CU.
 struct WinLds {
   uint4 hdr[HC][64];             // header windows (stage_window)
   uint4 desc[2][64];             // descriptors of tile t (buffer t & 1) and t + 1
 };
-static_assert(sizeof(WinLds) == 10240, "sixteen waves per CU");
+static_assert(sizeof(WinLds) == 10240, "10 KiB a wave");
 constexpr int WIN_U4 = (int)(sizeof(WinLds) / 16);
+constexpr int OCC_U4 = (int)((OCC_LDS_BYTES + 15) / 16);
 
 // Lane k < 32: how many lanes of `valid` have reason k (five ballots of the
 // reason's bits; the lane's own bits select each ballot or its complement).
@@ -2439,10 +2500,22 @@ __device__ __forceinline__ uint32_t reason_hist(uint32_t reason, bool valid, uin
 // tiles holding a frame with a body -- the pending words (uncounted: an
 // operation the count leaves out only makes a wait stricter).
 __device__ __forceinline__ void window_loop(const KParams& P) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_W * WIN_U4];
+  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_W * WIN_U4 + OCC_U4];
   const int wave = (int)(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u;
   WinLds& L = reinterpret_cast<WinLds*>(smem)[wave];
+  // The block's copy of the occupancy bitmaps and hwport bytes (before any
+  // LDS-DMA; the host sends only tables that fit, OCC_LDS_MAX4 / _MAX6).
+  uint32_t* const occ = reinterpret_cast<uint32_t*>(smem + WAVES_W * WIN_U4);
+  {
+    const uint32_t n4 = (P.ip4_mask + 32u) >> 5, n6 = (P.ip6_mask + 32u) >> 5;
+    for (uint32_t i = threadIdx.x; i < n4; i += WAVES_W * 64) occ[i] = P.occ4[i];
+    for (uint32_t i = threadIdx.x; i < n6; i += WAVES_W * 64) occ[OCC_LDS_B6 / 4 + i] = P.occ6[i];
+    if (threadIdx.x < 8)
+      occ[OCC_LDS_HW / 4 + threadIdx.x] = reinterpret_cast<const uint32_t*>(P.hwport)[threadIdx.x];
+    __syncthreads();
+  }
+  const uint32_t lds_occ = (uint32_t)(uintptr_t)(lptr)occ;
   const uint32_t gwave = sreg(blockIdx.x * WAVES_W + wave);
   const uint32_t W = gridDim.x * WAVES_W;
   if (gwave == 0) zero_claim_set(P.claim_next, lane);
@@ -2497,7 +2570,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
 
     // ---- lookups and the record.
-    Parsed ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
+    Parsed ps = demux_packet<true>(P, h, dv.intf_i, dv.abase, dv.span, dv.shift, lds_occ);
     const uint32_t reason = ps.r.reason;
     store_records(P, tile, ps.r, lane);
     // The pending words of a tile holding frames with a body.
