@@ -1760,24 +1760,13 @@ __device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, ui
   return desc_at(P, lane < t.cnt ? t.first + lane : lane % P.n);
 }
 
-__device__ __forceinline__ void lds_write16(void* p, const uint4& v) {
-  const u32x4 w = {v.x, v.y, v.z, v.w};
-  asm volatile("ds_write_b128 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(w) : "memory");
-}
-
 // Stages the tile's header windows for the parse.  Rows 0..HC-1 hold the
 // windows packet-major: packet p's 128-B window is row-major at byte 128 p,
 // its cell k at 16 * ((k - p) & 7) within it, so one LDS-DMA instruction
 // reads eight packets' windows, eight lanes (one 128-B run) per packet --
 // 8-16 cache lines per instruction, not 64 -- and the packet-per-lane reads
-// of any one cell fall in distinct banks.  Chunks a frame does not have
-// read zeros: from the zero region, or (ZLDS, win_kernel) written into LDS
-// (ds_write), which for short frames halves the window loads' cache-line
-// traffic -- what the CU's texture units are busy with there (DESIGN.md §5
-// round 4; rx_kernel has no VGPRs for it).  Lane 0 of a row always loads
-// (its zero line when it has no chunk), so each row is one vector-memory
-// instruction, as the counted waits assume.  All lanes active.
-template <bool ZLDS = false>
+// of any one cell fall in distinct banks.  Chunks a frame does not have read
+// zeros.  All lanes active.
 __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64],
                                              uint32_t lane) {
   const uint32_t lo = (uint32_t)dv.abase, hi = (uint32_t)(dv.abase >> 32);
@@ -1797,13 +1786,7 @@ __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, 
     const uint32_t c = ((lane & 7u) + p) & 7u;
     const uint64_t ab = (uint64_t)h[i] << 32 | l[i];
     const int nwin = ((int)sp[i] + 15) >> 4;
-    const bool real = (int)c < nwin;
-    if (!ZLDS) {
-      glds<OO_RX_HDR_AUX>(real ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
-    } else {
-      if (real || lane == 0) glds<OO_RX_HDR_AUX>(real ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
-      if (!real && lane != 0) lds_write16(&rows[i][lane], make_uint4(0u, 0u, 0u, 0u));
-    }
+    glds<OO_RX_HDR_AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
   }
 }
 
@@ -2003,6 +1986,10 @@ __device__ __forceinline__ uint32_t tx_l4_check(const TxHdr& h, int shift, uint3
   return (h.udp && v == 0u) ? 0xffffu : v;
 }
 
+__device__ __forceinline__ void lds_write16(void* p, const uint4& v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(w) : "memory");
+}
 
 // The wave's NST_TX = 6 stores (tests/test_kernel_isa.py checks the code
 // object holds exactly these).  Frames in the whole-granule form (TxHdr):
@@ -2544,7 +2531,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
     vm_wait<0>();
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
-    stage_window<true>(d0, zero_line(P, t0, lane), L.hdr, lane);
+    stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
     glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   }
 
@@ -2577,7 +2564,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       const Unit nt = unit_of(P, tnext);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the parse's LDS reads are done
-      stage_window<true>(dn, zero_line(P, nt, lane), L.hdr, lane);
+      stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
     }
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
     claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
