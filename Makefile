@@ -21,7 +21,7 @@ HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 # tests/test_gpu_wait_variants.py runs parity on every build.
 CHECK_VARIANTS := r6e4:-DOO_RX_RING=6,-DOO_RX_EXTRA=4 r8e2:-DOO_RX_RING=8,-DOO_RX_EXTRA=2 \
                   w1e0:-DOO_RX_WAVES=1,-DOO_RX_EXTRA=0 rb6:-DOO_RX_BODY_RING=6 \
-                  rb12:-DOO_RX_BODY_RING=12,-DOO_RX_WIN_WPE=3
+                  rb12:-DOO_RX_BODY_RING=12
 CHECKS := $(foreach v,$(CHECK_VARIANTS),build/check/liboo_gpu_rx_$(firstword $(subst :, ,$(v))).so)
 
 all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling tools/ring_probe tools/poll_bench $(CHECKS)
