@@ -750,6 +750,9 @@ void apply_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
   c->grid_short = grid(c->bpc[1]);
   c->grid_win = grid(c->bpc[2]);
   c->grid_body = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]);
+#ifdef OO_RX_CONCUR  // (experiment: grid_pct sizes win_kernel only)
+  c->grid_body = (t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]) * c->ncu;
+#endif
   c->kmode = t->path;
   c->tstep = t->tstep == 1 ? 1 : 8;
   c->dyn = t->static_tiles == 0;
