@@ -222,12 +222,6 @@ struct oo_gpu_rx_ctx {
   uint64_t next_ticket = 1;
   std::vector<HostReg> regs;
   hipStream_t stream = nullptr;  // the context's own stream (setup work)
-#ifdef OO_RX_CONCUR
-  // Experiment (OO_RX_EXPERIMENTS builds): body_kernel on this stream,
-  // concurrent with win_kernel (fork / join events).
-  hipStream_t aux = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-#endif
   uint8_t* h_image_hdr = nullptr;  // pinned 64-B table image header
 };
 
@@ -560,11 +554,6 @@ void free_dev(oo_gpu_rx_ctx* c) {
   if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
   if (c->h_image_hdr) (void)hipHostFree(c->h_image_hdr);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-#ifdef OO_RX_CONCUR
-  if (c->aux) (void)hipStreamDestroy(c->aux);
-  if (c->fork) (void)hipEventDestroy(c->fork);
-  if (c->join) (void)hipEventDestroy(c->join);
-#endif
 }
 
 // An event that completes once everything enqueued on t's stream so far
@@ -750,9 +739,6 @@ void apply_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
   c->grid_short = grid(c->bpc[1]);
   c->grid_win = grid(c->bpc[2]);
   c->grid_body = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]);
-#ifdef OO_RX_CONCUR  // (experiment: grid_pct sizes win_kernel only)
-  c->grid_body = (t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]) * c->ncu;
-#endif
   c->kmode = t->path;
   c->tstep = t->tstep == 1 ? 1 : 8;
   c->dyn = t->static_tiles == 0;
@@ -1145,18 +1131,6 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   set_groups(A, WA, CLAIM_GROUPS, 0u);
   set_tiles_dyn(A, n, WA, c->body_tail, 1);
   A.dyn = B.dyn = 1u;
-#ifdef OO_RX_CONCUR
-  if ((c->aux == nullptr && (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-                             hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-                             hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess)) ||
-      hipEventRecord(c->fork, s) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork, 0) != hipSuccess)
-    return -EIO;
-  if (oo_rx_launch_body(&A, (int)blocks_a, c->aux) != 0) return -EIO;
-  if (oo_rx_launch_win(&B, (int)blocks_b, s) != 0) return -EIO;
-  if (hipEventRecord(c->join, c->aux) != hipSuccess || hipStreamWaitEvent(s, c->join, 0) != hipSuccess)
-    return -EIO;
-  return 0;
-#endif
   if (oo_rx_launch_win(&B, (int)blocks_b, s) != 0) return -EIO;
   if (oo_rx_launch_body(&A, (int)blocks_a, s) != 0) return -EIO;
   return 0;

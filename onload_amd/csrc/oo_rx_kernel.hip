@@ -189,7 +189,7 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
   return s;
 }
 
-#if (defined(OO_RX_STAMPS) || defined(OO_RX_CONCUR)) && !defined(OO_RX_EXPERIMENTS)
+#if defined(OO_RX_STAMPS) && !defined(OO_RX_EXPERIMENTS)
 #error "OO_RX_STAMPS is a diagnostic build (tools/build_ref.sh sets OO_RX_EXPERIMENTS)"
 #endif
 #ifdef OO_RX_STAMPS
@@ -2661,9 +2661,7 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
   const uint32_t gwave = sreg(blockIdx.x * WAVES_B + wave);
   const uint32_t W = gridDim.x * WAVES_B;
   // No frame of the batch waits for its body: nothing to do.
-#ifndef OO_RX_CONCUR
   if (__hip_atomic_load(P.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-#endif
   if (gwave >= P.ntiles) return;
   uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
   if (lane == 0) {
@@ -2685,11 +2683,7 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     const uint64_t zero = zero_line(P, unit, lane);
     // Jobs: the frames with a body whose verdict waits for it.
     const uint32_t tgt = plo & 0xffffu;
-#ifdef OO_RX_CONCUR  // (timing experiment: every frame with a body, no verdicts)
-    const bool job = dv.valid && dv.span > HB;
-#else
     const bool job = dv.valid && dv.span > HB && tgt != PEND_NONE;
-#endif
     uint32_t myslot;
     const Jobs J = jobs_setup(dv.abase, job ? dv.span : 0, lane, myslot);
     const uint32_t fm = min_x8(J.nb);
@@ -2760,11 +2754,7 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     }
 
     // ---- verdicts: a failing sum turns the record into the drop record.
-#ifdef OO_RX_CONCUR
-    const bool fail = job && (res16(bsum) ^ tgt) == 0x1234u;  // (kept live; results wrong)
-#else
     const bool fail = job && res16(bsum) != tgt;
-#endif
     if (__ballot(fail) != 0) {
       if (fail) {
         const bool tcp = (plo >> 16) & 1u;
