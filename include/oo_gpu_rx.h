@@ -275,7 +275,10 @@ int oo_gpu_rx_set_len_hint(oo_gpu_rx_ctx* ctx, uint32_t mean_frame_len);
  * measured fastest.  The library reads no environment: a deployment gets
  * exactly these defaults unless it calls this.  0 or -EINVAL. */
 typedef struct oo_gpu_rx_tuning {
-  uint32_t path;           /* 0 auto; 1 one rx_kernel launch, 4-slot body ring;
+  uint32_t path;           /* 0 auto (frames within the 128-B header window,
+                              2^20+ packets: 3; else 2 for under 1 KiB of
+                              buffer per packet, 1 otherwise);
+                              1 one rx_kernel launch, 4-slot body ring;
                               2 the same with the 2-slot ring; 3 the split
                               transform (win_kernel + body_kernel)            */
   uint32_t grid_pct;       /* % of the resident grid to launch (0: 100)       */

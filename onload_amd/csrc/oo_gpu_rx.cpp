@@ -1189,7 +1189,14 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // only for tables that fit there (oo_rx_kernel.hip OCC_LDS_MAX4 / _MAX6).
   const bool split_fits = (uint64_t)c->ip4_mask + 1 <= oo_rx::OCC_LDS_MAX4 &&
                           (uint64_t)c->ip6_mask + 1 <= oo_rx::OCC_LDS_MAX6;
-  if (!tx && c->kmode == 3 && split_fits && c->grid_win > 0 && c->grid_body > 0) {
+  // Auto: batches whose frames fit the 128-B header window (by the hint, or
+  // at most 128 buffer bytes per packet) take it from 2^20 packets on --
+  // win_kernel alone does their work (config 3 -9 %);
+  // body_kernel finds nothing and returns.  Smaller batches keep one launch.
+  const bool window_frames =
+      c->len_hint ? c->len_hint <= (uint32_t)oo_rx::HB_BYTES : P.frames_bytes <= (uint64_t)oo_rx::HB_BYTES * n;
+  const bool split = c->kmode == 3 || (c->kmode == 0 && window_frames && n >= (1u << 20));
+  if (!tx && split && split_fits && c->grid_win > 0 && c->grid_body > 0) {
     const int rc = launch_split(c, P, n, trk, P.claim, s);
     if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
     trk->parity ^= 1u;

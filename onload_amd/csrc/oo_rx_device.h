@@ -156,6 +156,8 @@ constexpr uint32_t OCC_LDS_HW = 8192 + 2048;
 constexpr uint32_t OCC_LDS_BYTES = OCC_LDS_HW + 32;
 constexpr uint32_t OCC_LDS_MAX4 = 1u << 16, OCC_LDS_MAX6 = 1u << 14;
 constexpr uint32_t FLAG_LINE = 2 * CLAIM_GROUPS;
+// The staged header window per packet (oo_rx_kernel.hip HB).
+constexpr uint32_t HB_BYTES = 128;
 
 // The split transform's pending word of a frame with a body (KParams::pend,
 // 8 B per packet, written by win_kernel, read by body_kernel):

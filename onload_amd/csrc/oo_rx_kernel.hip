@@ -80,6 +80,7 @@ constexpr int R = OO_RX_RING;
 static_assert(R % 2 == 0, "rx_kernel consumes its ring two pieces at a time");
 constexpr int HC = 8;                // staged header chunks per packet
 constexpr int HB = HC * 16;          // staged window bytes per packet
+static_assert(HB == (int)HB_BYTES, "oo_rx_device.h HB_BYTES");
 
 constexpr uint32_t PENDING = 0xffu;
 
@@ -2516,12 +2517,6 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     __syncthreads();
   }
   const uint32_t lds_occ = (uint32_t)(uintptr_t)(lptr)occ;
-  // The window cells a frame does not have read one zero cell per tile (one
-  // line for the whole row instruction, not eight: fewer L1 accesses).
-#ifndef OO_RX_WIN_ZERO1
-#define OO_RX_WIN_ZERO1 1
-#endif
-  const uint32_t WZL = OO_RX_WIN_ZERO1 ? 0u : lane;
   const uint32_t gwave = sreg(blockIdx.x * WAVES_W + wave);
   const uint32_t W = gridDim.x * WAVES_W;
   if (gwave == 0) zero_claim_set(P.claim_next, lane);
@@ -2537,7 +2532,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
     vm_wait<0>();
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
-    stage_window(d0, zero_line(P, t0, WZL), L.hdr, lane);
+    stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
     glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   }
 
@@ -2570,7 +2565,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       const Unit nt = unit_of(P, tnext);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the parse's LDS reads are done
-      stage_window(dn, zero_line(P, nt, WZL), L.hdr, lane);
+      stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
     }
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
     claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
