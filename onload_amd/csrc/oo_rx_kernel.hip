@@ -432,43 +432,6 @@ __device__ __forceinline__ Rec load_rec(const KParams& P, const PR& t, uint32_t 
   return r;
 }
 
-// The first records of an IPv4-only wave (32 B each), two lanes per record:
-// the first load fetches the records of the even lanes (lane 2k its d0,
-// lane 2k+1 its d1), the second those of the odd lanes, and one lane swap
-// gives every lane its own record.  Each load then touches 32 lines, not 64:
-// half the L1 accesses of one record per lane per load, on the texture
-// path config 3 is bound by.  All lanes active; want:
-// this lane needs its record (slot i).
-#ifndef OO_RX_REC_PAIRS
-#define OO_RX_REC_PAIRS 1
-#endif
-__device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ uint4 swap_pair4(const uint4& v) {
-  return make_uint4(swap_pair(v.x), swap_pair(v.y), swap_pair(v.z), swap_pair(v.w));
-}
-template <class PR>
-__device__ __forceinline__ Rec load_rec_pairs(const PR& t, uint32_t i, bool want) {
-  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const bool odd = (lane & 1u) != 0;
-  const uint64_t a = t.slots + ((uint64_t)i << 5);
-  const uint64_t pa = (uint64_t)swap_pair((uint32_t)a) | ((uint64_t)swap_pair((uint32_t)(a >> 32)) << 32);
-  const bool pwant = swap_pair(want ? 1u : 0u) != 0u;
-  // first load: the even lane's record; second: the odd lane's
-  const uint64_t a1 = odd ? pa + 16u : a, a2 = odd ? a + 16u : pa;
-  const bool w1 = odd ? pwant : want, w2 = odd ? want : pwant;
-  uint4 x1 = make_uint4(0u, 0u, 0u, 0u), x2 = x1;
-  if (w1) x1 = gload16(a1);
-  if (w2) x2 = gload16(a2);
-  const uint4 s1 = swap_pair4(x1), s2 = swap_pair4(x2);
-  Rec r;
-  r.d0 = odd ? s2 : x1;
-  r.d1 = odd ? x2 : s1;
-  r.d2 = r.d3 = make_uint4(0u, 0u, 0u, 0u);
-  return r;
-}
-
 // One visited slot against the lookup key:
 //  IPv4 (handle_entry, netif_table.c:192-231): the first probe matches only
 //   an OCCUPIED_PREFERRED entry and its lport is implied (LPRP, hash.h:76-163,
@@ -1265,10 +1228,7 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     // when this one did not match.
     const int fs = o0 ? 0 : o1 ? 1 : o2 ? 2 : 3;
     Rec rec = {};
-    if (OO_RX_REC_PAIRS && !ANY6 && LO)
-      rec = load_rec_pairs(t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, look && fs < 3);
-    else if (look && fs < 3)
-      rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
+    if (look && fs < 3) rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
     if (look) {
       DSTAMP(9);
       // Both families walk in one instruction stream (lookup_stages<2>).
