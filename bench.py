@@ -338,6 +338,7 @@ def run_rank(args) -> None:
                       "counts_match": ok, "path": group_path}
     counts = ctr.cpu().numpy()
     assert counts.sum() == n_total, counts
+    path = stack.last_path()  # which kernels the timed launches ran
 
     bytes_all = torch.tensor([float(buf.nbytes), float(desc["len"].astype(np.float64).sum())],
                              dtype=torch.float64, device=dev)
@@ -418,6 +419,7 @@ def run_rank(args) -> None:
                        else "count"},
             "gbps": round(gbs, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "kernels": PATH_KERNELS.get(path, []),
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 5),
                          "kernel_ms_max_rank": round(kern_ms_max, 5),
@@ -433,6 +435,12 @@ def run_rank(args) -> None:
         if group is not None:
             group.close()
         dist.destroy_process_group()
+
+
+# oo_gpu_rx_last_path -> the kernels one timed launch runs (their summed
+# duration is the launch's; rocprofv3 lists them separately).
+PATH_KERNELS = {1: ["oo_rx::rx_kernel"], 2: ["oo_rx_short::rx_kernel"],
+                3: ["oo_rx::win_kernel", "oo_rx::body_kernel"]}
 
 
 def time_scatter(torch, dist, shards, cfg, seed, n_total, rank, world, dev, my_buf,

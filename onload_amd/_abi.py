@@ -154,6 +154,7 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_sync_tables": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_stream_done": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_table_gen": (ctypes.c_uint64, [_P]),
+    "oo_gpu_rx_last_path": (ctypes.c_uint32, [_P]),
     "oo_gpu_rx_set_len_hint": (ctypes.c_int, [_P, _U32]),
     "oo_gpu_rx_set_tuning": (ctypes.c_int, [_P, ctypes.POINTER(Tuning)]),
     "oo_gpu_rx_process_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _P]),

@@ -191,6 +191,7 @@ struct oo_gpu_rx_ctx {
   uint32_t gen = 1;       // flush generation (sockgen marks)
   uint32_t tables_gen = 0;  // flushes done; streams wait for it via tables_ev
   uint64_t changes = 0;     // table / socket changes made (oo_gpu_rx_table_gen)
+  uint32_t last_path = 0;   // the last RX batch's kernels (oo_gpu_rx_last_path)
   hipEvent_t tables_ev = nullptr;
   hipStream_t tables_stream = nullptr;
   OpStage stage[2];
@@ -943,6 +944,8 @@ int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* c, int32_t id, const oo_gpu_rx_sock* s) {
 
 uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* c) { return c == nullptr ? 0 : c->changes; }
 
+uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* c) { return c == nullptr ? 0 : c->last_path; }
+
 int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   if (c == nullptr) return -EINVAL;
   if (!has_dev(c)) return -ENODEV;
@@ -1200,6 +1203,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
     const int rc = launch_split(c, P, n, trk, P.claim, s);
     if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
     trk->parity ^= 1u;
+    c->last_path = 3;
     note_launch(trk);
     return 0;
   }
@@ -1240,7 +1244,10 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
                     : use_short ? oo_rx_launch_short(&P, grid, s) : oo_rx_launch(&P, grid, s);
   if (rc != 0) return -EIO;  // (nothing ran: the set stays zero for the next launch)
   trk->parity ^= 1u;
-  if (!tx) note_launch(trk);
+  if (!tx) {
+    note_launch(trk);
+    c->last_path = use_short ? 2u : 1u;
+  }
   return 0;
 }
 

@@ -190,6 +190,15 @@ class GpuRxStack:
         if rc:
             raise OSError(-rc, "oo_gpu_rx_sync_tables")
 
+    def table_gen(self) -> int:
+        """oo_gpu_rx_table_gen: table and socket changes made so far."""
+        return int(self._lib.oo_gpu_rx_table_gen(self._ctx))
+
+    def last_path(self) -> int:
+        """oo_gpu_rx_last_path: the last batch's kernels (1 / 2 rx_kernel
+        instances, 3 the split transform, 0 none yet)."""
+        return int(self._lib.oo_gpu_rx_last_path(self._ctx))
+
     def set_len_hint(self, mean_frame_len: int) -> None:
         """Mean frame length of the batches to come (0: inferred from the
         buffer bytes per packet); picks the kernel instance."""

@@ -163,6 +163,7 @@ def test_full_size_config2_bit_exact(cuda):
     g, o = _pair(lambda s: s.load_world(filters, socks))
     buf, desc = pktgen.generate(2, 1 << 20)
     got = _check(g, o, buf, desc)
+    assert g.last_path() == 1  # long frames: rx_kernel, 4-slot ring
     frac = np.bincount(got["reason"], minlength=32) / len(got)
     assert abs(frac[_abi.R_UDP_CSUM] - 0.01) < 0.002
     assert abs(frac[_abi.R_NO_MATCH] - 0.005) < 0.002
@@ -175,6 +176,7 @@ def test_full_size_config3_bit_exact(cuda):
     g, o = _pair(lambda s: s.load_world(filters, socks))
     buf, desc = pktgen.generate(3, 1 << 24, nthreads=NTHREADS)
     got = _check(g, o, buf, desc)
+    assert g.last_path() == 3  # window-sized frames, 2^20+: the split transform
     assert (got["stage"][got["reason"] == 0] == 2).all()
 
 
