@@ -5,8 +5,10 @@
   python tools/pmc_summary.py --config 2 --dir gpurun_out/ev2/pmc_c2 [--out profiles/pmc_config2.json]
 
 Each pass directory (fetch/, write/, sq/, tcc/) holds one rocprofv3 run with
---kernel-trace and its counters; values are averaged over the rx_kernel
-launches.  FETCH_SIZE is doubled: on gfx950 it counts a 128-B request as 64 B
+--kernel-trace and its counters; values are averaged over each kernel's
+launches and summed over the kernels one batch runs (--kernels, or the bench
+line's roofline.kernels: rx_kernel, or win_kernel + body_kernel for the split
+transform).  FETCH_SIZE is doubled: on gfx950 it counts a 128-B request as 64 B
 (MI355X_MICROARCH.md, HBM/rocprofv3 section); WRITE_SIZE is taken as read.
 Both are in KiB."""
 from __future__ import annotations
@@ -27,7 +29,7 @@ def counters(path: str, kernel: str = "rx_kernel") -> dict:
     vals: dict = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if kernel not in r["Kernel_Name"]:
+            if not r["Kernel_Name"].startswith(kernel + "("):
                 continue
             key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), r["Counter_Name"])
             vals.setdefault(r["Counter_Name"], {}).setdefault(key[0], 0.0)
@@ -42,15 +44,27 @@ def main() -> None:
     ap.add_argument("--out")
     ap.add_argument("--bench-json", help="a bench.py line of the same configuration: "
                     "its roofline.achieved x kernel_ms gives the algorithmic bytes")
+    ap.add_argument("--kernels", help="comma-separated kernel names (default: the bench "
+                    "line's roofline.kernels, else oo_rx::rx_kernel)")
     a = ap.parse_args()
     from bench import DEFAULT_N  # noqa: E402
+    bench = None
+    if a.bench_json:
+        line = [x for x in open(a.bench_json).read().splitlines() if x.startswith("{")][-1]
+        bench = json.loads(line)
+    kernels = (a.kernels.split(",") if a.kernels else
+               (bench or {}).get("roofline", {}).get("kernels") or ["oo_rx::rx_kernel"])
     res = {"config": a.config, "packets_per_launch": DEFAULT_N[a.config],
-           "kernel": "oo_rx::rx_kernel"}
-    allc = {}
+           "kernel": " + ".join(kernels)}
+    allc: dict = {}
     for p in sorted(os.listdir(a.dir)):
         d = os.path.join(a.dir, p)
-        if os.path.isdir(d):
-            allc.update(counters(d))
+        if not os.path.isdir(d):
+            continue
+        for k in kernels:
+            for name, (v, n) in counters(d, k).items():
+                tot, cnt = allc.get(name, (0.0, 0))
+                allc[name] = (tot + v, max(cnt, n))
     for name, (v, n) in sorted(allc.items()):
         res[name] = v
         res[name + "_launches"] = n
@@ -58,9 +72,8 @@ def main() -> None:
         rd = allc["FETCH_SIZE"][0] * 2 * 1024
         wr = allc["WRITE_SIZE"][0] * 1024
         alg = None
-        if a.bench_json:
-            line = [x for x in open(a.bench_json).read().splitlines() if x.startswith("{")][-1]
-            r = json.loads(line)["roofline"]
+        if bench is not None:
+            r = bench["roofline"]
             alg = r["achieved"] * r["kernel_ms"] * 1e6
         res.update({
             "correction": "FETCH_SIZE x2 (gfx950 counts 128-B requests as 64 B, MI355X_MICROARCH.md "
