@@ -363,6 +363,21 @@ static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs
   c->n = n;
   c->busy = 0;
   c->st = *base;
+  if( p->cfg.flags & OO_RX_POLL_CROSSOVER ) {
+    /* Priced first with every event transformed: the device's side of the
+     * model only gains with more frames, so a chunk that loses even then
+     * goes back at once, unclassified. */
+    for( i = 0; i < n; ++i )
+      total += evs[i].len;
+    if( !gpu_pays(p, n, total) ) {
+      for( i = 0; i < n; ++i )
+        c->what[i] = W_OTHER;
+      c->st.n_handback += n;
+      c->m = 0;
+      return 0;
+    }
+    total = 0;
+  }
   for( i = 0; i < n; ++i ) {
     c->what[i] = (uint8_t)classify(p, &evs[i], &c->st);
     if( c->what[i] == W_TRANSFORM ) {

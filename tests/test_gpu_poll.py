@@ -215,3 +215,53 @@ def test_poll_table_change_in_a_callback(cuda, evs_per_poll):
     assert p.stats.n_batches == n // evs_per_poll + 1  # + the rest (the next chunk: replaced)
     p.close()
     g.close()
+
+
+@pytest.mark.parametrize("zero_copy", (False, True))
+def test_poll_crossover(cuda, zero_copy):
+    """OO_RX_POLL_CROSSOVER (oo_rx_poll.c gpu_pays): a chunk the cost model
+    prices below the device batch goes back whole, in order, through
+    other_ev (the call site runs it through the per-event loop), counted only
+    in n_handback; a chunk it prices above runs exactly as without the flag.
+    Chunks of one poll are priced one by one: with evs_per_poll 64 and a
+    model whose fixed cost 40 frames of the corpus repay, the short last
+    chunk goes back and the full ones do not."""
+    rng = np.random.default_rng(11)
+    frames = edge_frames(seed=11)
+    pool, evs = events_for(frames, BUF, rng)
+    n = len(evs)
+
+    def run(crossover, epp=64):
+        g = GpuRxStack(device=0, intf_hwport=HWPORTS, host_stage_bytes=64 << 20,
+                       host_stage_pkts=65536)
+        install(g, edge_world())
+        rec = Recorder()
+        p = poll.RxPoll(g, pool, BUF, epp, True, rec, zero_copy=zero_copy, crossover=crossover)
+        assert p.poll(evs) == n
+        st = p.stats.as_dict()
+        p.close()
+        g.close()
+        return rec, st
+
+    base_rec, base_st = run(None)
+    # never pays: everything handed back, nothing else counted
+    rec, st = run({"gpu_fixed_ns": 1 << 30})
+    assert rec.calls == [("other", int(e["rq_id"])) for e in evs]
+    assert st["n_handback"] == n and st["n_batches"] == 0
+    assert all(v == 0 for k, v in st.items() if k != "n_handback"), st
+    # always pays: the same calls, records and counters as without the flag
+    rec, st = run({"cpu_pkt_ps": 1 << 30})
+    assert rec.calls == base_rec.calls
+    assert [r.tobytes() if hasattr(r, "tobytes") else r for r in rec.recs] == \
+        [r.tobytes() if hasattr(r, "tobytes") else r for r in base_rec.recs]
+    assert st == base_st
+    # per chunk: fixed = 40 frames' worth of the CPU's per-frame saving
+    per = {"cpu_pkt_ps": 20000, "cpu_byte_ps": 0, "gpu_pkt_ps": 10000, "gpu_byte_ps": 0,
+           "gpu_fixed_ns": 400}
+    rec, st = run(per)
+    cut = (n // 64) * 64
+    if n - cut < 40:
+        tail = [("other", int(e["rq_id"])) for e in evs[cut:]]
+        assert rec.calls[len(rec.calls) - len(tail):] == tail
+        assert st["n_handback"] == n - cut
+    assert st["n_batches"] >= (cut // 64) - 1
