@@ -222,7 +222,8 @@ def test_poll_crossover(cuda, zero_copy):
     """OO_RX_POLL_CROSSOVER (oo_rx_poll.c gpu_pays): a chunk the cost model
     prices below the device batch goes back whole, in order, through
     other_ev (the call site runs it through the per-event loop), counted only
-    in n_handback; a chunk it prices above runs exactly as without the flag.
+    in n_handback and n_other (every event other_ev receives); a chunk it
+    prices above runs exactly as without the flag.
     Chunks of one poll are priced one by one: with evs_per_poll 64 and a
     model whose fixed cost 40 frames of the corpus repay, the short last
     chunk goes back and the full ones do not."""
@@ -247,8 +248,8 @@ def test_poll_crossover(cuda, zero_copy):
     # never pays: everything handed back, nothing else counted
     rec, st = run({"gpu_fixed_ns": 1 << 30})
     assert rec.calls == [("other", int(e["rq_id"])) for e in evs]
-    assert st["n_handback"] == n and st["n_batches"] == 0
-    assert all(v == 0 for k, v in st.items() if k != "n_handback"), st
+    assert st["n_handback"] == n and st["n_other"] == n and st["n_batches"] == 0
+    assert all(v == 0 for k, v in st.items() if k not in ("n_handback", "n_other")), st
     # always pays: the same calls, records and counters as without the flag
     rec, st = run({"cpu_pkt_ps": 1 << 30})
     assert rec.calls == base_rec.calls
