@@ -13,7 +13,7 @@ for c in ${CONFIGS:-2 3 4 5}; do
   timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 5 $extra \
     > "$OUT/bench_c$c.json" 2> "$OUT/bench_c$c.err" || { tail -5 "$OUT/bench_c$c.err"; exit 1; }
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c$c" -o run --output-format csv \
-     -- python3 "$ROOT/bench.py" --config $c --steps 20 --warmup 5 --no-cpu-baseline \
+     -- python3 "$ROOT/bench.py" --config $c --steps 20 --warmup 5 --steady 0 --no-cpu-baseline \
      > "$OUT/prof_c$c.log" 2>&1) || { tail -5 "$OUT/prof_c$c.log"; exit 1; }
   for pass in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $pass -d "$OUT/pmc_c$c/$pass" -o run \
