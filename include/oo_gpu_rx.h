@@ -295,6 +295,9 @@ typedef struct oo_gpu_rx_tuning {
   uint32_t tstep;          /* static partition tile-size step: 1, else 8      */
   uint32_t body_bpc;       /* body_kernel blocks per CU at most (0: all that fit) */
   uint32_t body_tail;      /* body_kernel unit at the batch's end, packets (0: 16) */
+  uint32_t body_engine;    /* body_kernel: 0 by frame size (per-group job
+                              sequences for frames under 1 KiB of buffer,
+                              else lockstep slots), 1 lockstep, 2 sequences */
 } oo_gpu_rx_tuning;
 int oo_gpu_rx_set_tuning(oo_gpu_rx_ctx* ctx, const oo_gpu_rx_tuning* t);
 

@@ -75,7 +75,8 @@ class Tuning(ctypes.Structure):
                 ("groups", ctypes.c_uint32), ("gshift", ctypes.c_int32),
                 ("static_tiles", ctypes.c_uint32), ("tail_tile", ctypes.c_uint32),
                 ("tail_per_wave", ctypes.c_uint32), ("tstep", ctypes.c_uint32),
-                ("body_bpc", ctypes.c_uint32), ("body_tail", ctypes.c_uint32)]
+                ("body_bpc", ctypes.c_uint32), ("body_tail", ctypes.c_uint32),
+                ("body_engine", ctypes.c_uint32)]
 
 
 #: The measurement settings tests and tools pass through the environment of
@@ -83,7 +84,8 @@ class Tuning(ctypes.Structure):
 TUNING_ENV = {"OO_RX_KERNEL": "path", "OO_RX_GRID_PCT": "grid_pct", "OO_RX_GROUPS": "groups",
               "OO_RX_GSHIFT": "gshift", "OO_RX_STATIC": "static_tiles",
               "OO_RX_TAIL_TILE": "tail_tile", "OO_RX_TAIL_PER_WAVE": "tail_per_wave",
-              "OO_RX_TSTEP": "tstep", "OO_RX_BODY_BPC": "body_bpc", "OO_RX_BODY_TAIL": "body_tail"}
+              "OO_RX_TSTEP": "tstep", "OO_RX_BODY_BPC": "body_bpc", "OO_RX_BODY_TAIL": "body_tail",
+              "OO_RX_BODY_ENGINE": "body_engine"}
 
 
 def tuning_from_env() -> "Tuning | None":

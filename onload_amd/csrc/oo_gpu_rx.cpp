@@ -42,6 +42,8 @@ extern "C" int oo_rx_win_waves_per_block(void);
 extern "C" int oo_rx_body_waves_per_block(void);
 extern "C" int oo_rx_launch_win(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_rx_launch_body(const oo_rx::KParams* P, int grid, hipStream_t stream);
+extern "C" int oo_rx_body_blocks_per_cu_gseq(void);
+extern "C" int oo_rx_launch_body_gseq(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
                                    const uint32_t* d_lev_end, uint32_t nlev, uint32_t gen,
                                    hipStream_t s);
@@ -208,9 +210,11 @@ struct oo_gpu_rx_ctx {
   uint32_t gshift = ~0u;       // claim group of a wave: (gwave >> gshift) mod groups (~0u: per launch)
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t grid_short = 0;     // resident blocks of the short-frame rx_kernel (0: unused)
-  uint32_t ncu = 0, bpc[4] = {0, 0, 0, 0};  // CUs; resident blocks per CU of the four kernels
+  uint32_t ncu = 0, bpc[5] = {0, 0, 0, 0, 0};  // CUs; resident blocks per CU of the five kernels
   uint32_t grid_win = 0;       // resident blocks of win_kernel (split transform)
   uint32_t grid_body = 0;      // resident blocks of body_kernel
+  uint32_t grid_body_gseq = 0; // ... of its per-group-sequence instance
+  uint32_t body_engine = 0;    // oo_gpu_rx_tuning::body_engine
   uint32_t body_tail = 16;     // packets per body_kernel unit at the batch's end
   uint32_t kmode = 0;          // rx kernel: 0 by frame size, 1 always the 4-slot, 2 always the 2-slot
   uint32_t len_hint = 0;       // mean frame length of the batches to come (0: from buffer bytes)
@@ -740,6 +744,8 @@ void apply_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
   c->grid_short = grid(c->bpc[1]);
   c->grid_win = grid(c->bpc[2]);
   c->grid_body = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]);
+  c->grid_body_gseq = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[4]) : c->bpc[4]);
+  c->body_engine = t->body_engine;
   c->kmode = t->path;
   c->tstep = t->tstep == 1 ? 1 : 8;
   c->dyn = t->static_tiles == 0;
@@ -757,7 +763,7 @@ extern "C" {
 int oo_gpu_rx_abi_version(void) { return OO_GPU_RX_ABI_VERSION; }
 
 int oo_gpu_rx_set_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
-  if (c == nullptr || (t != nullptr && (t->path > 3 || t->grid_pct > 100))) return -EINVAL;
+  if (c == nullptr || (t != nullptr && (t->path > 3 || t->grid_pct > 100 || t->body_engine > 2))) return -EINVAL;
   apply_tuning(c, t);
   return 0;
 }
@@ -805,9 +811,9 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) {
     // Persistent grids: every resident block (occupancy query).
     c->ncu = (uint32_t)prop.multiProcessorCount;
-    const int b[4] = {oo_rx_blocks_per_cu(), oo_rx_blocks_per_cu_short(), oo_rx_win_blocks_per_cu(),
-                      oo_rx_body_blocks_per_cu()};
-    for (int k = 0; k < 4; ++k) c->bpc[k] = (uint32_t)std::max(0, b[k]);
+    const int b[5] = {oo_rx_blocks_per_cu(), oo_rx_blocks_per_cu_short(), oo_rx_win_blocks_per_cu(),
+                      oo_rx_body_blocks_per_cu(), oo_rx_body_blocks_per_cu_gseq()};
+    for (int k = 0; k < 5; ++k) c->bpc[k] = (uint32_t)std::max(0, b[k]);
   }
   apply_tuning(c, nullptr);
   DevTables& T = c->T;
@@ -1104,7 +1110,11 @@ static void set_tiles_dyn(KParams& P, uint32_t n, uint64_t W, uint32_t S, uint32
 // then body_kernel, on s.  The stream's pending-word buffer grows in stream
 // order (hipMallocAsync), so no call waits for the device.
 static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Tracked* trk,
-                        uint32_t* set, hipStream_t s) {
+                        uint32_t* set, hipStream_t s, bool short_frames) {
+  // Mixed sizes are the short-frame class's (IMIX): its body engine runs
+  // per-group job sequences, which idle less of the ring on them.
+  const bool gseq = c->body_engine ? c->body_engine == 2 : short_frames;
+  const uint32_t grid_body = gseq ? c->grid_body_gseq : c->grid_body;
   if (trk->pend_n < (uint64_t)n + 64) {
     if (trk->pend != nullptr && hipFreeAsync(trk->pend, s) != hipSuccess) return -EIO;
     trk->pend = nullptr;
@@ -1127,7 +1137,7 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   // body_kernel: stream-bound units (64 single-wave groups), a finer tail.
   const uint32_t wpb_b = (uint32_t)oo_rx_body_waves_per_block();
   const uint32_t blocks_a =
-      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + wpb_b - 1) / wpb_b, c->grid_body));
+      std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + wpb_b - 1) / wpb_b, grid_body));
   const uint64_t WA = (uint64_t)blocks_a * (uint32_t)oo_rx_body_waves_per_block();
   A.claim = set + 32u * CLAIM_GROUPS;
   A.claim_next = nullptr;
@@ -1135,7 +1145,8 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   set_tiles_dyn(A, n, WA, c->body_tail, 1);
   A.dyn = B.dyn = 1u;
   if (oo_rx_launch_win(&B, (int)blocks_b, s) != 0) return -EIO;
-  if (oo_rx_launch_body(&A, (int)blocks_a, s) != 0) return -EIO;
+  if ((gseq ? oo_rx_launch_body_gseq(&A, (int)blocks_a, s) : oo_rx_launch_body(&A, (int)blocks_a, s)) != 0)
+    return -EIO;
   return 0;
 }
 
@@ -1199,8 +1210,8 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   const bool window_frames =
       c->len_hint ? c->len_hint <= (uint32_t)oo_rx::HB_BYTES : P.frames_bytes <= (uint64_t)oo_rx::HB_BYTES * n;
   const bool split = c->kmode == 3 || (c->kmode == 0 && window_frames && n >= (1u << 20));
-  if (!tx && split && split_fits && c->grid_win > 0 && c->grid_body > 0) {
-    const int rc = launch_split(c, P, n, trk, P.claim, s);
+  if (!tx && split && split_fits && c->grid_win > 0 && c->grid_body > 0 && c->grid_body_gseq > 0) {
+    const int rc = launch_split(c, P, n, trk, P.claim, s, short_frames);
     if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
     trk->parity ^= 1u;
     c->last_path = 3;

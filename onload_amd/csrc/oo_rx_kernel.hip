@@ -2449,10 +2449,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
 // -s4 - sigma pseudo (mod M) (sigma^2 == 1 mod M).  s4 is the window part
 // as the parse leaves it, possibly negative ("Why the split sum is exact";
 // |s4| < 2^31: at most a 64-KiB frame's words).
+#endif  // !OO_RX_SHORT
 __device__ __forceinline__ uint32_t res16(uint32_t x) {  // x mod 0xffff
   const uint32_t f = fold16(x);
   return f == 0xffffu ? 0u : f;
 }
+#ifndef OO_RX_SHORT
 __device__ __forceinline__ uint32_t body_target(uint32_t s4, uint32_t pseudo, bool odd) {
   const int32_t sv = (int32_t)s4;
   const uint32_t r4 = sv >= 0 ? res16((uint32_t)sv) : (0xffffu - res16((uint32_t)(-(int64_t)sv))) % 0xffffu;
@@ -2601,6 +2603,7 @@ __global__ __launch_bounds__(WAVES_W * 64) __attribute__((amdgpu_waves_per_eu(OO
     KParams P) {
   window_loop(P);
 }
+#endif  // !OO_RX_SHORT
 
 // ---------------------------------------------------------------------------
 // body_kernel: units of up to 64 packets (its own partition, finer at the
@@ -2687,7 +2690,9 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     const bool job = dv.valid && dv.span > HB && tgt != PEND_NONE;
     uint32_t myslot;
     const Jobs J = jobs_setup(dv.abase, job ? dv.span : 0, lane, myslot);
+#if !OO_RX_GSEQ
     const uint32_t fm = min_x8(J.nb);
+#endif
 
     // ---- stage the unit after next (into this unit's buffers, now read)
     // and claim the one after that: older than this unit's rounds, so the
@@ -2703,9 +2708,34 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     const uint32_t T = (J.T + RB - 1) / RB * RB;
     uint32_t bsum = 0;
     if (T != 0) {
-      // issue side
       IssueCursor ci;
       issue_slot(ci, J, 0, lane, zero);
+#if OO_RX_GSEQ
+      // Per-group job sequences (the short-frame instance, mixed sizes):
+      // the tile loop's cursors.
+#pragma unroll
+      for (int u = 0; u < RB; ++u) issue_round(ci, J, zero, &L.ring[u][0], lane);
+      ConsumeCursor cc;
+      consume_start(cc, J, lane);
+      for (uint32_t k0 = 0; k0 < T; k0 += RB) {
+        const bool last = k0 + RB == T;
+#pragma unroll
+        for (int u = 0; u < RB; u += 2) {
+          if (last) vm_wait_n(RB - 2 - u);
+          else vm_wait<RB - 2>();
+          uint4 v0, v1;
+          lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
+          consume_round(cc, J, v0, lane);
+          consume_round(cc, J, v1, lane);
+          if (!last) {
+            issue_round(ci, J, zero, &L.ring[u][0], lane);
+            issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
+          }
+        }
+      }
+      bsum = lane_get(cc.bs, myslot);
+#else
+      // issue side
       uint32_t fi = slot_full(fm, 0);
       auto issue = [&](void* slot) {
         glds<OO_RX_BODY_AUX>(ci.a, slot);
@@ -2752,6 +2782,7 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
         }
       }
       bsum = lane_get(cc.bs, myslot);
+#endif
     }
 
     // ---- verdicts: a failing sum turns the record into the drop record.
@@ -2786,7 +2817,6 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
 }
 
 __global__ __launch_bounds__(WAVES_B * 64) void body_kernel(KParams P) { body_loop(P); }
-#endif
 
 }  // namespace oo_rx
 
@@ -2802,6 +2832,19 @@ extern "C" int oo_rx_blocks_per_cu_short(void) {
 // Launch one RX batch of short frames on `stream`.
 extern "C" int oo_rx_launch_short(const oo_rx::KParams* P, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(oo_rx_short::rx_kernel, dim3(grid), dim3(oo_rx_short::WAVES * 64), 0, stream, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The split transform's body_kernel with per-group job sequences (mixed
+// frame sizes).
+extern "C" int oo_rx_body_blocks_per_cu_gseq(void) {
+  int b = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx_short::body_kernel,
+                                                                     oo_rx_short::WAVES_B * 64, 0);
+  return e == hipSuccess ? b : 0;
+}
+extern "C" int oo_rx_launch_body_gseq(const oo_rx::KParams* P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx_short::body_kernel, dim3(grid), dim3(oo_rx_short::WAVES_B * 64), 0, stream, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #else

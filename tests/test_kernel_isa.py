@@ -130,6 +130,16 @@ def test_split_kernels_no_scratch(asm):
     assert _usage(stderr, BODY)["VGPRs"] <= 128
 
 
+def test_gseq_body_kernel_no_scratch(asm_short):
+    """body_kernel with per-group job sequences (the short-frame instance)."""
+    text, stderr = asm_short
+    k = "_ZN11oo_rx_short11body_kernelEN5oo_rx7KParamsE"
+    u = _usage(stderr, k)
+    assert u["VGPRs Spill"] == 0, u
+    assert "scratch_" not in _body(text, k)
+    assert not re.findall(r"flat_store|flat_load|flat_atomic", _body(text, k))
+
+
 def test_split_store_counts(asm):
     text, _ = asm
     w = _body(text, WIN)
