@@ -2657,6 +2657,160 @@ __device__ __forceinline__ void stage_unit(const KParams& P, const Unit& u, uint
   __builtin_amdgcn_global_load_lds(reinterpret_cast<gptr>(pa + 4u), (lptr)(&L.pend[b][1][0]), 4, 0, 0);
 }
 
+// The verdicts of one unit: a failing sum turns the record into the drop
+// record (only the fields a drop defines), the per-reason counts move.
+__device__ __forceinline__ void unit_verdicts(const KParams& P, BodyLds& L, bool job, uint32_t bsum,
+                                              uint32_t plo, uint32_t phi, uint32_t idx) {
+  const bool fail = job && res16(bsum) != (plo & 0xffffu);
+  if (__ballot(fail) != 0) {
+    if (fail) {
+      const bool tcp = (plo >> 16) & 1u;
+      const uint32_t reason = tcp ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+      const uint4 r0 = make_uint4(reason | (((plo >> 17) & 3u) << 8) | ((tcp ? 6u : 17u) << 24),
+                                  phi & 0xffffu, phi >> 16, 0u);
+      const uint4 r1 = make_uint4(0u, 0u, 0xffffffffu, 0u);
+      uint4* const o = reinterpret_cast<uint4*>(P.out) + 2ull * idx;
+      o[0] = r0;
+      o[1] = r1;
+      if (P.counters != nullptr) {
+        lds_add4(&L.cnt[(plo >> 24) & (OO_RX_R_COUNT - 1)], 0xffffffffu);
+        lds_add4(&L.cnt[reason], 1u);
+      }
+    }
+  }
+}
+
+#if OO_RX_GSEQ
+// One unit as the continuous stream sees it: its jobs and what its verdicts
+// need.
+struct BUnit {
+  Jobs J;
+  uint32_t myslot, plo, phi, idx;
+  bool job;
+  uint64_t zero;
+  uint32_t T;  // rounds, a multiple of RB (0: no job)
+};
+__device__ __forceinline__ BUnit bunit_read(const KParams& P, BodyLds& L, uint32_t b, uint32_t t,
+                                            uint32_t lane) {
+  BUnit U;
+  const Unit unit = unit_of(P, t);
+  const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), unit, lane);
+  U.plo = lds_read4(&L.pend[b][0][lane]);
+  U.phi = lds_read4(&L.pend[b][1][lane]);
+  U.idx = dv.idx;
+  U.zero = zero_line(P, unit, lane);
+  U.job = dv.valid && dv.span > HB && (U.plo & 0xffffu) != PEND_NONE;
+  U.J = jobs_setup(dv.abase, U.job ? dv.span : 0, lane, U.myslot);
+  U.T = (U.J.T + RB - 1) / RB * RB;
+  return U;
+}
+
+// body_loop with per-group job sequences and one continuous stream: the
+// ring is not drained at a unit's end -- its last turn issues the first
+// rounds of the next unit, whose jobs were set up at the unit's start -- so
+// a wave pays the memory latency once per run of units with bodies, not
+// once per unit.  Each iteration reads the next unit's descriptors and
+// pending words (staged one unit earlier), stages the unit after it into the
+// buffer the current unit was read from, and claims the one after that.
+__device__ __forceinline__ void body_loop(const KParams& P) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_B * BODY_U4];
+  const int wave = (int)(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  BodyLds& L = reinterpret_cast<BodyLds*>(smem)[wave];
+  const uint32_t gwave = sreg(blockIdx.x * WAVES_B + wave);
+  const uint32_t W = gridDim.x * WAVES_B;
+  // No frame of the batch waits for its body: nothing to do.
+  if (__hip_atomic_load(P.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  if (gwave >= P.ntiles) return;
+  uint32_t tcur = gwave, tnext = gwave + W, tnext2 = gwave + 2u * W, got = 0;
+  if (lane == 0) {
+    const uint32_t g = group_of(P, gwave);
+    lds_write4(&L.dbase, 3u * W + g);
+    lds_write4(&L.gofs, 32u * g);
+  }
+  if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
+  stage_unit(P, unit_of(P, tcur), lane, L, 0);
+  stage_unit(P, unit_of(P, tnext), lane, L, 1);
+  vm_wait<0>();
+
+  BUnit C = bunit_read(P, L, 0, tcur, lane);
+  IssueCursor ci;
+  ConsumeCursor cc;
+  if (C.T != 0) {
+    issue_slot(ci, C.J, 0, lane, C.zero);
+#pragma unroll
+    for (int u = 0; u < RB; ++u) issue_round(ci, C.J, C.zero, &L.ring[u][0], lane);
+  }
+  uint32_t b = 0;
+  // Vector-memory operations issued after the last staging when the
+  // iteration that issued it waited for none of them (a unit without jobs):
+  // its claim, and the next unit's first rounds if it primed them.
+  int unwaited = 0;
+  for (uint32_t it_ = 0; tcur < P.ntiles; b ^= 1u, ++it_) {
+    // ---- the next unit (staged in buffer b ^ 1 one iteration ago: landed
+    // once that iteration's waits passed rounds issued after it), then the
+    // unit after it staged into buffer b (read one iteration ago) and the one
+    // after that claimed: all older than the rounds the waits below count.
+    if (unwaited != 0) vm_wait_n(unwaited - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const BUnit N = bunit_read(P, L, b ^ 1u, tnext, lane);
+    if (it_ != 0) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+      tnext2 = P.dyn ? sreg(lds_read4(&L.dbase)) + c : tnext2 + W;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage_unit(P, unit_of(P, tnext2), lane, L, b);
+    claim_tile(P.claim + sreg(lds_read4(&L.gofs)), P.ngroups, lane, got);
+
+    uint32_t bsum = 0;
+    unwaited = C.T != 0 ? 0 : 2;  // (the claim; +RB below)
+    if (C.T != 0) {
+      IssueCursor ni;  // the next unit's first rounds go out in this unit's last turn
+      const bool carry = N.T != 0;
+      if (carry) issue_slot(ni, N.J, 0, lane, N.zero);
+      consume_start(cc, C.J, lane);
+      for (uint32_t k0 = 0; k0 < C.T; k0 += RB) {
+        const bool last = k0 + RB == C.T;
+#pragma unroll
+        for (int u = 0; u < RB; u += 2) {
+          if (last && !carry) vm_wait_n(RB - 2 - u);
+          else vm_wait<RB - 2>();
+          uint4 v0, v1;
+          lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
+          consume_round(cc, C.J, v0, lane);
+          consume_round(cc, C.J, v1, lane);
+          if (!last) {
+            issue_round(ci, C.J, C.zero, &L.ring[u][0], lane);
+            issue_round(ci, C.J, C.zero, &L.ring[u + 1][0], lane);
+          } else if (carry) {
+            issue_round(ni, N.J, N.zero, &L.ring[u][0], lane);
+            issue_round(ni, N.J, N.zero, &L.ring[u + 1][0], lane);
+          }
+        }
+      }
+      bsum = lane_get(cc.bs, C.myslot);
+      if (carry) ci = ni;
+    } else if (N.T != 0) {  // nothing here: start the next unit's stream
+      issue_slot(ci, N.J, 0, lane, N.zero);
+#pragma unroll
+      for (int u = 0; u < RB; ++u) issue_round(ci, N.J, N.zero, &L.ring[u][0], lane);
+      unwaited += RB;
+    }
+    unit_verdicts(P, L, C.job, bsum, C.plo, C.phi, C.idx);
+    C = N;
+    tcur = tnext;
+    tnext = tnext2;
+  }
+  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (P.counters != nullptr) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (ln < OO_RX_R_COUNT) {
+      const uint32_t c = lds_read4(&L.cnt[ln]);
+      if (c != 0) atomicAdd(&P.counters[ln], c);
+    }
+  }
+}
+#else
 __device__ __forceinline__ void body_loop(const KParams& P) {
   __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_B * BODY_U4];
   const int wave = (int)(threadIdx.x >> 6);
@@ -2690,9 +2844,7 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     const bool job = dv.valid && dv.span > HB && tgt != PEND_NONE;
     uint32_t myslot;
     const Jobs J = jobs_setup(dv.abase, job ? dv.span : 0, lane, myslot);
-#if !OO_RX_GSEQ
     const uint32_t fm = min_x8(J.nb);
-#endif
 
     // ---- stage the unit after next (into this unit's buffers, now read)
     // and claim the one after that: older than this unit's rounds, so the
@@ -2710,31 +2862,6 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     if (T != 0) {
       IssueCursor ci;
       issue_slot(ci, J, 0, lane, zero);
-#if OO_RX_GSEQ
-      // Per-group job sequences (the short-frame instance, mixed sizes):
-      // the tile loop's cursors.
-#pragma unroll
-      for (int u = 0; u < RB; ++u) issue_round(ci, J, zero, &L.ring[u][0], lane);
-      ConsumeCursor cc;
-      consume_start(cc, J, lane);
-      for (uint32_t k0 = 0; k0 < T; k0 += RB) {
-        const bool last = k0 + RB == T;
-#pragma unroll
-        for (int u = 0; u < RB; u += 2) {
-          if (last) vm_wait_n(RB - 2 - u);
-          else vm_wait<RB - 2>();
-          uint4 v0, v1;
-          lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
-          consume_round(cc, J, v0, lane);
-          consume_round(cc, J, v1, lane);
-          if (!last) {
-            issue_round(ci, J, zero, &L.ring[u][0], lane);
-            issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
-          }
-        }
-      }
-      bsum = lane_get(cc.bs, myslot);
-#else
       // issue side
       uint32_t fi = slot_full(fm, 0);
       auto issue = [&](void* slot) {
@@ -2782,27 +2909,9 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
         }
       }
       bsum = lane_get(cc.bs, myslot);
-#endif
     }
 
-    // ---- verdicts: a failing sum turns the record into the drop record.
-    const bool fail = job && res16(bsum) != tgt;
-    if (__ballot(fail) != 0) {
-      if (fail) {
-        const bool tcp = (plo >> 16) & 1u;
-        const uint32_t reason = tcp ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
-        const uint4 r0 = make_uint4(reason | (((plo >> 17) & 3u) << 8) | ((tcp ? 6u : 17u) << 24),
-                                    phi & 0xffffu, phi >> 16, 0u);
-        const uint4 r1 = make_uint4(0u, 0u, 0xffffffffu, 0u);
-        uint4* const o = reinterpret_cast<uint4*>(P.out) + 2ull * dv.idx;
-        o[0] = r0;
-        o[1] = r1;
-        if (P.counters != nullptr) {
-          lds_add4(&L.cnt[(plo >> 24) & (OO_RX_R_COUNT - 1)], 0xffffffffu);
-          lds_add4(&L.cnt[reason], 1u);
-        }
-      }
-    }
+    unit_verdicts(P, L, job, bsum, plo, phi, dv.idx);
     tcur = tnext;
     tnext = tnext2;
   }
@@ -2815,6 +2924,8 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     }
   }
 }
+
+#endif  // OO_RX_GSEQ
 
 __global__ __launch_bounds__(WAVES_B * 64) void body_kernel(KParams P) { body_loop(P); }
 
