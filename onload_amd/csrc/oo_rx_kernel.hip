@@ -1044,6 +1044,9 @@ __device__ __forceinline__ Match lookup_stages(const KParams& P, const PR& t, bo
 #ifndef OO_RX_FSM
 #define OO_RX_FSM 1
 #endif
+#ifndef OO_RX_FSM2
+#define OO_RX_FSM2 1  // win_kernel: two slots per load level (lookup_fsm2)
+#endif
 template <int M, class PR>
 __device__ __forceinline__ Match lookup_fsm(const KParams& P, const PR& t, bool any6,
                                             const Hdr& h, uint32_t dport, uint32_t sport,
@@ -1137,6 +1140,122 @@ __device__ __forceinline__ Match lookup_fsm(const KParams& P, const PR& t, bool 
     }
   }
   DSTAMPV(11, 1000000u + guard);  // the wave's steps (marked: not a time)
+  return m;
+}
+
+// The state machine with the occupancy bits in LDS (win_kernel): every
+// step also loads the record of the next slot on the lane's probe sequence
+// when that slot is occupied, and evaluates it in the same step when the
+// walk goes on to it -- two slots per dependent load along a chain (config
+// 5's connected-socket chains).  The same walks,
+// matches and stages as lookup_fsm; EMPTY slots are known from LDS before
+// any load, so no record of an EMPTY slot is loaded.
+template <int M>
+__device__ __forceinline__ Match lookup_fsm2(const KParams& P, const ProbeL& t, bool any6,
+                                             const Hdr& h, uint32_t dport, uint32_t sport,
+                                             uint32_t proto, uint32_t hwp, int vlan, bool tcp,
+                                             uint32_t h1_0, uint32_t h1_1, uint32_t h1_2,
+                                             uint32_t h2_0, uint32_t h2_1, uint32_t h2_2, bool o1,
+                                             bool o2, Rec rec, int fs, int& stage, bool& s2) {
+  const uint32_t nst = tcp ? 3u : 2u;  // o2 is false for UDP
+  const bool six = M == 1 || (M == 2 && t.is6);
+  Match m = {-1, 0};
+  bool probe = false;
+  s2 = false;
+  uint32_t s = (uint32_t)fs;
+  bool live = s < nst;
+  uint32_t h1 = s == 0 ? h1_0 : s == 1 ? h1_1 : h1_2;
+  uint32_t first = h1;
+  uint32_t h2 = s == 0 ? h2_0 : s == 1 ? h2_1 : h2_2;
+  uint32_t k = 0;
+  bool occ = true;  // slot h1 not EMPTY (rec is its record)
+  // The second record: slot (h1 + h2) & mask, when it is occupied and not
+  // the cycle's start.
+  Rec rec2 = {};
+  bool have2 = false;
+  {
+    const uint32_t n = (h1 + h2) & t.mask;
+    have2 = live && n != first && probe_occ(P, t, n);
+    if (have2) rec2 = load_rec(P, t, n, any6);
+  }
+  for (uint32_t guard = 0; __ballot(live) != 0 && guard <= 3u * (t.mask + 1u); ++guard) {
+    if (live) {
+      bool end = !occ;  // an EMPTY slot ends the stage's walk
+      // Up to two slots of the same walk: rec (slot h1), then rec2.
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool eval = e == 0 ? !end : (!end && have2);
+        if (eval) {
+          const bool st0 = s == 0;
+          uint32_t la[4], ra[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            la[i] = s < 2 ? h.da[i] : 0u;
+            ra[i] = st0 ? h.sa[i] : 0u;
+          }
+          int32_t id;
+          if (rec_match_m<M>(P, t, e == 0 ? rec : rec2, k == 0, la, dport, ra, !st0,
+                             st0 ? sport : 0u, proto, hwp, vlan, id)) {
+            if (probe) {
+              s2 = true;
+              end = true;
+            } else {
+              if (m.n == 0) m.first = id;
+              ++m.n;
+              end = tcp;  // TCP's deliver callbacks end the walk at the first match
+            }
+          }
+          if (!end) {
+            h1 = (h1 + h2) & t.mask;
+            end = h1 == first;  // a full cycle
+            ++k;
+            // the next slot: its record came with this batch, or it is
+            // EMPTY (or, after the second record, not loaded yet)
+            if (!end && !(e == 0 && have2)) end = !probe_occ(P, t, h1);
+          }
+        }
+      }
+      if (end) {
+        if (probe) {
+          live = false;
+        } else if (m.n != 0) {
+          stage = (int)s + 1;  // this stage decides
+          live = false;
+          if (!tcp && !six && s == 0 && m.n == 1 && o1) {
+            probe = true;  // and stage 2 is walked for the future rule
+            live = true;
+            s = 1;
+            h1 = h1_1;
+            first = h1;
+            h2 = h2_1;
+            k = 0;
+          }
+        } else {
+          ++s;
+          if (s == 1 && !o1) ++s;
+          if (s == 2 && !o2) ++s;
+          live = s < nst;
+          h1 = s == 1 ? h1_1 : h1_2;
+          first = h1;
+          h2 = s == 1 ? h2_1 : h2_2;
+          k = 0;
+        }
+      }
+      // The records of slot h1 and the one after it, occupied ones only
+      // (after two slots, h1 may be occupied without its record: it is
+      // loaded here).
+      have2 = false;
+      if (live) {
+        occ = probe_occ(P, t, h1);
+        if (occ) {
+          rec = load_rec(P, t, h1, any6);
+          const uint32_t n = (h1 + h2) & t.mask;
+          have2 = n != first && probe_occ(P, t, n);
+          if (have2) rec2 = load_rec(P, t, n, any6);
+        }
+      }
+    }
+  }
   return m;
 }
 
@@ -1234,7 +1353,19 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
       // Both families walk in one instruction stream (lookup_stages<2>).
       // Waves with TCP lookups (three stages, long connected-socket chains)
       // take the state machine; UDP-only waves the stage-by-stage walks.
-      if (OO_RX_FSM && any_tcp)
+      if constexpr (LO) {
+        if (OO_RX_FSM2 && any_tcp)
+          m = lookup_fsm2<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, hwp, vlan, tcp, h1_0, h1_1,
+                                        h1_2, h2_0, h2_1, h2_2, o1, o2, rec, fs, stage, s2);
+        else if (OO_RX_FSM && any_tcp)
+          m = lookup_fsm<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, hwp, vlan, tcp, h1_0, h1_1,
+                                       h1_2, h2_0, h2_1, h2_2, o0, o1, o2, q0, q1, q2, rec, fs, stage,
+                                       s2);
+        else
+          m = lookup_stages<ANY6 ? 2 : 0, !ANY6>(P, t, any6, h, dport, sport, proto, hwp, vlan, tcp,
+                                                 h1_0, h1_1, h1_2, o0, o1, o2, q0, q1, q2, rec, fs,
+                                                 stage, s2);
+      } else if (OO_RX_FSM && any_tcp)
         m = lookup_fsm<ANY6 ? 2 : 0>(P, t, any6, h, dport, sport, proto, hwp, vlan, tcp, h1_0, h1_1,
                                      h1_2, h2_0, h2_1, h2_2, o0, o1, o2, q0, q1, q2, rec, fs, stage,
                                      s2);
