@@ -1900,7 +1900,7 @@ __device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, ui
 // of any one cell fall in distinct banks.  Chunks a frame does not have read
 // zeros.  All lanes active.
 __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64],
-                                             uint32_t lane) {
+                                             uint32_t lane, bool masked = false) {
   const uint32_t lo = (uint32_t)dv.abase, hi = (uint32_t)(dv.abase >> 32);
   // Every row's frame fields first (24 permutes, one wait), then the eight
   // DMAs: fetched row by row, each row waited for its own permutes.
@@ -1918,7 +1918,10 @@ __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, 
     const uint32_t c = ((lane & 7u) + p) & 7u;
     const uint64_t ab = (uint64_t)h[i] << 32 | l[i];
     const int nwin = ((int)sp[i] + 15) >> 4;
-    glds<OO_RX_HDR_AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
+    // masked (wave-uniform): cells 4..7 already hold zeros and no frame has
+    // them -- those lanes issue nothing (lane 0 reads cell 0: every row is
+    // still one instruction).
+    if (!masked || c < 4u) glds<OO_RX_HDR_AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
   }
 }
 
@@ -2659,6 +2662,12 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
   uint32_t cnt = 0;    // lane k < 32: this wave's count of reason k
   bool waits = false;  // a frame of this wave's tiles waits for its body
 
+  // Window positions of cells 4..7 all zero (the last staged tile had no
+  // frame past 64 bytes): a tile of such frames then stages cells 0..3 only.
+#ifndef OO_RX_WIN_MASKED
+#define OO_RX_WIN_MASKED 1
+#endif
+  bool clean = false;
   // Prologue: tile t0's descriptors and windows, then t1's descriptors.
   {
     const Unit t0 = unit_of(P, tcur);
@@ -2666,6 +2675,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     vm_wait<0>();
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
     stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
+    clean = __ballot(d0.span > 64) == 0;
     glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   }
 
@@ -2698,7 +2708,9 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       const Unit nt = unit_of(P, tnext);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the parse's LDS reads are done
-      stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
+      const bool short4 = __ballot(dn.span > 64) == 0;
+      stage_window(dn, zero_line(P, nt, lane), L.hdr, lane, OO_RX_WIN_MASKED && clean && short4);
+      clean = short4;
     }
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
     claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
