@@ -2618,6 +2618,9 @@ constexpr int OCC_U4 = (int)((OCC_LDS_BYTES + 15) / 16);
 __device__ __forceinline__ uint32_t reason_hist(uint32_t reason, bool valid, uint32_t lane) {
   static_assert(OO_RX_R_COUNT == 32, "five reason bits");
   uint64_t m = __ballot(valid);
+  // (the common tile: every packet delivered -- one count, in lane 0)
+  if (__ballot(valid && reason != OO_RX_R_DELIVER) == 0)
+    return lane == 0 ? (uint32_t)__popcll(m) : 0u;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
     const uint64_t bj = __ballot((reason >> j) & 1u);
