@@ -1644,8 +1644,10 @@ struct ConsumeCursor {
   uint32_t bs;          // the total of job (group, lane & 7); 0 if none
 };
 
+// mtab: an LDS table of the 17 byte masks by valid-byte count (body_kernel),
+// or nullptr: computed.
 __device__ __forceinline__ void consume_job(ConsumeCursor& c, const Jobs& J, uint32_t js,
-                                            uint32_t lane) {
+                                            uint32_t lane, const uint4* mtab = nullptr) {
   const uint32_t gj = lane & 7u, s = (lane & ~7u) + min(js, 7u);
   const uint32_t nb0 = lane_get(J.nb, s), lim = lane_get(J.lim, s);
   const uint32_t nb = js < 8u ? nb0 : 0u;
@@ -1655,16 +1657,21 @@ __device__ __forceinline__ void consume_job(ConsumeCursor& c, const Jobs& J, uin
   c.klv = c.k + lv;
   const int last = 16 * (int)(gj + 8u * (lv - 1u));  // this lane's last chunk
   c.vb = (uint32_t)min(max((int)lim - last, 0), 16);
-  auto bytes = [](int k) -> uint32_t {
-    return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * k)) - 1u;
-  };
-  const int vb = (int)c.vb;
-  c.m = make_uint4(bytes(vb), bytes(vb - 4), bytes(vb - 8), bytes(vb - 12));
+  if (mtab != nullptr) {
+    c.m = lds_read16(&mtab[c.vb]);
+  } else {
+    auto bytes = [](int k) -> uint32_t {
+      return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * k)) - 1u;
+    };
+    const int vb = (int)c.vb;
+    c.m = make_uint4(bytes(vb), bytes(vb - 4), bytes(vb - 8), bytes(vb - 12));
+  }
 }
 
-__device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, uint32_t lane) {
+__device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, uint32_t lane,
+                                              const uint4* mtab = nullptr) {
   c.k = 0;
-  consume_job(c, J, 0, lane);
+  consume_job(c, J, 0, lane, mtab);
   c.acc = 0;
   c.bs = 0;
 }
@@ -1673,7 +1680,7 @@ __device__ __forceinline__ void consume_start(ConsumeCursor& c, const Jobs& J, u
 // their words by 0); a group whose job ends folds its eight lane sums into
 // the job's lane and moves on.
 __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, const uint4& v,
-                                              uint32_t lane) {
+                                              uint32_t lane, const uint4* mtab = nullptr) {
   const bool live = c.k < c.klv;
   const bool part = live && c.k + 1u == c.klv && c.vb != 16u;
   if (__ballot(part) == 0) {
@@ -1698,7 +1705,7 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
     const uint32_t t = group_sum8(c.acc);
     ConsumeCursor n;
     n.k = c.k;
-    consume_job(n, J, c.js + 1u, lane);
+    consume_job(n, J, c.js + 1u, lane, mtab);
     if (end) {
       if ((lane & 7u) == c.js) c.bs = t;
       c.acc = 0;
@@ -2770,11 +2777,28 @@ struct BodyLds {
   uint4 ring[RB][64];
   uint4 desc[2][64];             // descriptors of this unit and the next
   uint32_t pend[2][2][64];       // their pending words (low, high halves)
-  uint32_t cnt[OO_RX_R_COUNT];   // per-reason count changes
   uint32_t dbase, gofs, pad0, pad1;
 };
 static_assert(sizeof(BodyLds) % 16 == 0, "BodyLds is carved from a uint4 array");
 constexpr int BODY_U4 = (int)(sizeof(BodyLds) / 16);
+constexpr int MTAB_U4 = 17;  // the block's byte masks of a chunk by valid-byte count 0..16
+#ifndef OO_RX_BODY_MTAB
+#define OO_RX_BODY_MTAB 1  // the sequences engine takes its masks from the table
+#endif
+
+// The block's mask table (before any LDS-DMA; all threads, one barrier).
+__device__ __forceinline__ const uint4* body_mask_table(uint4* smem_tab) {
+  const uint32_t t = threadIdx.x;
+  if (t < (uint32_t)MTAB_U4) {
+    auto bytes = [](int k) -> uint32_t {
+      return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * k)) - 1u;
+    };
+    const int vb = (int)t;
+    smem_tab[t] = make_uint4(bytes(vb), bytes(vb - 4), bytes(vb - 8), bytes(vb - 12));
+  }
+  __syncthreads();
+  return smem_tab;
+}
 
 // min(v) over the lanes with the same lane & 7 (as max_x8).
 __device__ __forceinline__ uint32_t min_x8(uint32_t v) {
@@ -2805,7 +2829,7 @@ __device__ __forceinline__ void stage_unit(const KParams& P, const Unit& u, uint
 
 // The verdicts of one unit: a failing sum turns the record into the drop
 // record (only the fields a drop defines), the per-reason counts move.
-__device__ __forceinline__ void unit_verdicts(const KParams& P, BodyLds& L, bool job, uint32_t bsum,
+__device__ __forceinline__ void unit_verdicts(const KParams& P, bool job, uint32_t bsum,
                                               uint32_t plo, uint32_t phi, uint32_t idx) {
   const bool fail = job && res16(bsum) != (plo & 0xffffu);
   if (__ballot(fail) != 0) {
@@ -2818,9 +2842,9 @@ __device__ __forceinline__ void unit_verdicts(const KParams& P, BodyLds& L, bool
       uint4* const o = reinterpret_cast<uint4*>(P.out) + 2ull * idx;
       o[0] = r0;
       o[1] = r1;
-      if (P.counters != nullptr) {
-        lds_add4(&L.cnt[(plo >> 24) & (OO_RX_R_COUNT - 1)], 0xffffffffu);
-        lds_add4(&L.cnt[reason], 1u);
+      if (P.counters != nullptr) {  // (rare: one frame in a hundred)
+        atomicAdd(&P.counters[(plo >> 24) & (OO_RX_R_COUNT - 1)], 0xffffffffu);
+        atomicAdd(&P.counters[reason], 1u);
       }
     }
   }
@@ -2859,10 +2883,11 @@ __device__ __forceinline__ BUnit bunit_read(const KParams& P, BodyLds& L, uint32
 // pending words (staged one unit earlier), stages the unit after it into the
 // buffer the current unit was read from, and claims the one after that.
 __device__ __forceinline__ void body_loop(const KParams& P) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_B * BODY_U4];
+  __shared__ __attribute__((aligned(16))) uint4 smem[WAVES_B * BODY_U4 + MTAB_U4];
   const int wave = (int)(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u;
   BodyLds& L = reinterpret_cast<BodyLds*>(smem)[wave];
+  const uint4* const mtab = OO_RX_BODY_MTAB ? body_mask_table(smem + WAVES_B * BODY_U4) : nullptr;
   const uint32_t gwave = sreg(blockIdx.x * WAVES_B + wave);
   const uint32_t W = gridDim.x * WAVES_B;
   // No frame of the batch waits for its body: nothing to do.
@@ -2874,7 +2899,6 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     lds_write4(&L.dbase, 3u * W + g);
     lds_write4(&L.gofs, 32u * g);
   }
-  if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
   stage_unit(P, unit_of(P, tcur), lane, L, 0);
   stage_unit(P, unit_of(P, tnext), lane, L, 1);
   vm_wait<0>();
@@ -2914,7 +2938,7 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
       IssueCursor ni;  // the next unit's first rounds go out in this unit's last turn
       const bool carry = N.T != 0;
       if (carry) issue_slot(ni, N.J, 0, lane, N.zero);
-      consume_start(cc, C.J, lane);
+      consume_start(cc, C.J, lane, mtab);
       for (uint32_t k0 = 0; k0 < C.T; k0 += RB) {
         const bool last = k0 + RB == C.T;
 #pragma unroll
@@ -2923,8 +2947,8 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
           else vm_wait<RB - 2>();
           uint4 v0, v1;
           lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
-          consume_round(cc, C.J, v0, lane);
-          consume_round(cc, C.J, v1, lane);
+          consume_round(cc, C.J, v0, lane, mtab);
+          consume_round(cc, C.J, v1, lane, mtab);
           if (!last) {
             issue_round(ci, C.J, C.zero, &L.ring[u][0], lane);
             issue_round(ci, C.J, C.zero, &L.ring[u + 1][0], lane);
@@ -2942,18 +2966,10 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
       for (int u = 0; u < RB; ++u) issue_round(ci, N.J, N.zero, &L.ring[u][0], lane);
       unwaited += RB;
     }
-    unit_verdicts(P, L, C.job, bsum, C.plo, C.phi, C.idx);
+    unit_verdicts(P, C.job, bsum, C.plo, C.phi, C.idx);
     C = N;
     tcur = tnext;
     tnext = tnext2;
-  }
-  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  if (P.counters != nullptr) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (ln < OO_RX_R_COUNT) {
-      const uint32_t c = lds_read4(&L.cnt[ln]);
-      if (c != 0) atomicAdd(&P.counters[ln], c);
-    }
   }
 }
 #else
@@ -2973,7 +2989,6 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
     lds_write4(&L.dbase, 3u * W + g);
     lds_write4(&L.gofs, 32u * g);
   }
-  if (lane < OO_RX_R_COUNT) lds_write4(&L.cnt[lane], 0u);
   stage_unit(P, unit_of(P, tcur), lane, L, 0);
   stage_unit(P, unit_of(P, tnext), lane, L, 1);
   vm_wait<0>();
@@ -3057,17 +3072,9 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
       bsum = lane_get(cc.bs, myslot);
     }
 
-    unit_verdicts(P, L, job, bsum, plo, phi, dv.idx);
+    unit_verdicts(P, job, bsum, plo, phi, dv.idx);
     tcur = tnext;
     tnext = tnext2;
-  }
-  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  if (P.counters != nullptr) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (ln < OO_RX_R_COUNT) {
-      const uint32_t c = lds_read4(&L.cnt[ln]);
-      if (c != 0) atomicAdd(&P.counters[ln], c);
-    }
   }
 }
 
