@@ -1906,6 +1906,7 @@ __device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, ui
 // 8-16 cache lines per instruction, not 64 -- and the packet-per-lane reads
 // of any one cell fall in distinct banks.  Chunks a frame does not have read
 // zeros.  All lanes active.
+template <int AUX = OO_RX_HDR_AUX>
 __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, uint4 (*rows)[64],
                                              uint32_t lane, bool masked = false) {
   const uint32_t lo = (uint32_t)dv.abase, hi = (uint32_t)(dv.abase >> 32);
@@ -1928,7 +1929,7 @@ __device__ __forceinline__ void stage_window(const DescView& dv, uint64_t zero, 
     // masked (wave-uniform): cells 4..7 already hold zeros and no frame has
     // them -- those lanes issue nothing (lane 0 reads cell 0: every row is
     // still one instruction).
-    if (!masked || c < 4u) glds<OO_RX_HDR_AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
+    if (!masked || c < 4u) glds<AUX>((int)c < nwin ? ab + (uint64_t)c * 16 : zero, &rows[i][0]);
   }
 }
 
@@ -2677,6 +2678,12 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
 #ifndef OO_RX_WIN_MASKED
 #define OO_RX_WIN_MASKED 1
 #endif
+// The window rows nontemporal here (read once; no body stream to share the
+// L2 with): config 3 -1.7 % (rx_kernel keeps the default policy, +11 % on
+// config 2 with nontemporal header rows).
+#ifndef OO_RX_WIN_HDR_AUX
+#define OO_RX_WIN_HDR_AUX 2
+#endif
   bool clean = false;
   // Prologue: tile t0's descriptors and windows, then t1's descriptors.
   {
@@ -2684,7 +2691,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
     vm_wait<0>();
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
-    stage_window(d0, zero_line(P, t0, lane), L.hdr, lane);
+    stage_window<OO_RX_WIN_HDR_AUX>(d0, zero_line(P, t0, lane), L.hdr, lane);
     clean = __ballot(d0.span > 64) == 0;
     glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   }
@@ -2719,7 +2726,8 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the parse's LDS reads are done
       const bool short4 = __ballot(dn.span > 64) == 0;
-      stage_window(dn, zero_line(P, nt, lane), L.hdr, lane, OO_RX_WIN_MASKED && clean && short4);
+      stage_window<OO_RX_WIN_HDR_AUX>(dn, zero_line(P, nt, lane), L.hdr, lane,
+                                      OO_RX_WIN_MASKED && clean && short4);
       clean = short4;
     }
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
