@@ -2678,9 +2678,11 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
 #ifndef OO_RX_WIN_MASKED
 #define OO_RX_WIN_MASKED 1
 #endif
-// The window rows nontemporal here (read once; no body stream to share the
-// L2 with): config 3 -1.7 % (rx_kernel keeps the default policy, +11 % on
-// config 2 with nontemporal header rows).
+// The window rows of a tile whose frames all fit their windows are read
+// nontemporal (read once, no body pass after them): config 3 -1.7 %.  A
+// tile with longer frames keeps the default policy: body_kernel reads the
+// rest of those lines (nontemporal there: config 5 +5 %; rx_kernel likewise
+// keeps it, +11 % on config 2 with nontemporal header rows).
 #ifndef OO_RX_WIN_HDR_AUX
 #define OO_RX_WIN_HDR_AUX 2
 #endif
@@ -2691,7 +2693,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
     vm_wait<0>();
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
-    stage_window<OO_RX_WIN_HDR_AUX>(d0, zero_line(P, t0, lane), L.hdr, lane);
+    stage_window<OO_RX_HDR_AUX>(d0, zero_line(P, t0, lane), L.hdr, lane);
     clean = __ballot(d0.span > 64) == 0;
     glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   }
@@ -2726,8 +2728,11 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the parse's LDS reads are done
       const bool short4 = __ballot(dn.span > 64) == 0;
-      stage_window<OO_RX_WIN_HDR_AUX>(dn, zero_line(P, nt, lane), L.hdr, lane,
-                                      OO_RX_WIN_MASKED && clean && short4);
+      if (__ballot(dn.span > HB) == 0)  // no frame of the tile has a body
+        stage_window<OO_RX_WIN_HDR_AUX>(dn, zero_line(P, nt, lane), L.hdr, lane,
+                                        OO_RX_WIN_MASKED && clean && short4);
+      else
+        stage_window<OO_RX_HDR_AUX>(dn, zero_line(P, nt, lane), L.hdr, lane, false);
       clean = short4;
     }
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
