@@ -232,10 +232,11 @@ int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* ctx, void* stream);
  * compares it across its own callbacks to learn whether a batch submitted
  * before them was transformed on tables that have since changed. */
 uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* ctx);
-/* Which kernels transformed the context's last batch (oo_gpu_rx_tuning
- * path numbering: 1 rx_kernel with the 4-slot ring, 2 the 2-slot instance,
- * 3 the split transform win_kernel + body_kernel; 0 none yet).  For
- * measurements: which kernels a timed launch's duration covers. */
+/* Which kernels transformed the context's last batch: 1 rx_kernel with the
+ * 4-slot ring, 2 its 2-slot instance, 3 the split transform (win_kernel +
+ * body_kernel with lockstep slots), 4 the split transform with the
+ * per-group-sequence body_kernel; 0 none yet.  For measurements: which
+ * kernels a timed launch's duration covers. */
 uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* ctx);
 /* Streams.  The context remembers the streams it launched on (nothing is
  * recorded per batch): a table change enqueues an event on each of them at

@@ -1214,7 +1214,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
     const int rc = launch_split(c, P, n, trk, P.claim, s, short_frames);
     if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
     trk->parity ^= 1u;
-    c->last_path = 3;
+    c->last_path = (c->body_engine ? c->body_engine == 2 : short_frames) ? 4u : 3u;
     note_launch(trk);
     return 0;
   }

@@ -176,7 +176,8 @@ def test_full_size_config3_bit_exact(cuda):
     g, o = _pair(lambda s: s.load_world(filters, socks))
     buf, desc = pktgen.generate(3, 1 << 24, nthreads=NTHREADS)
     got = _check(g, o, buf, desc)
-    assert g.last_path() == 3  # window-sized frames, 2^20+: the split transform
+    assert g.last_path() == 4  # window-sized frames, 2^20+: the split transform
+    # (short-frame class: the per-group-sequence body engine)
     assert (got["stage"][got["reason"] == 0] == 2).all()
 
 
