@@ -1132,7 +1132,7 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   const uint32_t blocks_b =
       std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + wpb_w - 1) / wpb_w, c->grid_win));
   const uint64_t WBl = (uint64_t)blocks_b * wpb_w;
-  set_groups(B, WBl, 32u, 4u);
+  set_groups(B, WBl, c->ngroups_max ? c->ngroups_max : 32u, c->gshift != ~0u ? c->gshift : 4u);
   set_tiles_dyn(B, n, WBl, c->tail_tile, c->tail_per_wave);
   // body_kernel: stream-bound units (64 single-wave groups), a finer tail.
   const uint32_t wpb_b = (uint32_t)oo_rx_body_waves_per_block();
