@@ -1126,13 +1126,14 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   KParams B = base, A = base;
   B.pend = A.pend = trk->pend;
   B.flag = A.flag = set + 32u * oo_rx::FLAG_LINE;
-  // win_kernel: header-bound tiles, many claims per us (32 groups of
-  // 16-wave runs, each over all eight XCDs).
+  // win_kernel: header-bound tiles, many claims per us (16 groups of
+  // 16-wave runs; against 32 groups: config 3 -1.4 %, two reps,
+  // profiles/r04/ab_win_claims_c3.log).
   const uint32_t wpb_w = (uint32_t)oo_rx_win_waves_per_block();
   const uint32_t blocks_b =
       std::max<uint32_t>(1, std::min<uint64_t>(((n + 63) / 64 + wpb_w - 1) / wpb_w, c->grid_win));
   const uint64_t WBl = (uint64_t)blocks_b * wpb_w;
-  set_groups(B, WBl, c->ngroups_max ? c->ngroups_max : 32u, c->gshift != ~0u ? c->gshift : 4u);
+  set_groups(B, WBl, c->ngroups_max ? c->ngroups_max : 16u, c->gshift != ~0u ? c->gshift : 4u);
   set_tiles_dyn(B, n, WBl, c->tail_tile, c->tail_per_wave);
   // body_kernel: stream-bound units (64 single-wave groups), a finer tail.
   const uint32_t wpb_b = (uint32_t)oo_rx_body_waves_per_block();
