@@ -1305,22 +1305,16 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     }
     uint32_t hwp = 0xffu;
     const bool tcp = proto == 6u;
-    // All the bits in one batch: six words, or four when no lane of the
-    // wave looks up TCP (UDP has no third stage, and no hashes for it).
-    const bool any_tcp = __ballot(look && tcp) != 0;
     const uint32_t h1_0 = hash3(dx, dport, sx, sport, proto) & t.mask;
     const uint32_t h1_1 = hash3(dx, dport, 0u, 0u, proto) & t.mask;
-#ifndef OO_RX_LAZY_H3
-#define OO_RX_LAZY_H3 1
-#endif
-    uint32_t h1_2 = 0u, h2_2 = 0u;
-    if (!OO_RX_LAZY_H3 || any_tcp) {
-      h1_2 = hash3(0u, dport, 0u, 0u, proto) & t.mask;
-      h2_2 = hash2(0u, dport, 0u, 0u, proto);
-    }
+    const uint32_t h1_2 = hash3(0u, dport, 0u, 0u, proto) & t.mask;
     const uint32_t h2_0 = hash2(dx, dport, sx, sport, proto);
     const uint32_t h2_1 = hash2(dx, dport, 0u, 0u, proto);
+    const uint32_t h2_2 = hash2(0u, dport, 0u, 0u, proto);
+    // All the bits in one batch: six words, or four when no lane of the
+    // wave looks up TCP (UDP has no third stage).
     bool o0 = false, o1 = false, o2 = false, q0 = false, q1 = false, q2 = false;
+    const bool any_tcp = __ballot(look && tcp) != 0;
     if (look) {
       const uint32_t idx[6] = {h1_0, h1_1, h1_2, (h1_0 + h2_0) & t.mask, (h1_1 + h2_1) & t.mask,
                                (h1_2 + h2_2) & t.mask};
