@@ -1178,13 +1178,6 @@ __device__ __forceinline__ Match lookup_fsm2(const KParams& P, const ProbeL& t, 
     have2 = live && n != first && probe_occ(P, t, n);
     if (have2) rec2 = load_rec(P, t, n, any6);
   }
-  // (M = 2: whether a live lane of the wave walks the IPv6 table -- its
-  // records were loaded at 64 B and take the IPv6 compare; without one, the
-  // step loads 32 B and compares IPv4 only)
-#ifndef OO_RX_FSM2_FAM
-#define OO_RX_FSM2_FAM 1
-#endif
-  bool a6 = (M == 2 && OO_RX_FSM2_FAM) ? __ballot(live && t.is6) != 0 : M != 0;
   for (uint32_t guard = 0; __ballot(live) != 0 && guard <= 3u * (t.mask + 1u); ++guard) {
     if (live) {
       bool end = !occ;  // an EMPTY slot ends the stage's walk
@@ -1201,13 +1194,8 @@ __device__ __forceinline__ Match lookup_fsm2(const KParams& P, const ProbeL& t, 
             ra[i] = st0 ? h.sa[i] : 0u;
           }
           int32_t id;
-          const Rec& rr = e == 0 ? rec : rec2;
-          const bool hit =
-              (M != 2 || a6) ? rec_match_m<M>(P, t, rr, k == 0, la, dport, ra, !st0, st0 ? sport : 0u,
-                                              proto, hwp, vlan, id)
-                             : rec_match_m<0>(P, t, rr, k == 0, la, dport, ra, !st0, st0 ? sport : 0u,
-                                              proto, hwp, vlan, id);
-          if (hit) {
+          if (rec_match_m<M>(P, t, e == 0 ? rec : rec2, k == 0, la, dport, ra, !st0,
+                             st0 ? sport : 0u, proto, hwp, vlan, id)) {
             if (probe) {
               s2 = true;
               end = true;
@@ -1257,15 +1245,14 @@ __device__ __forceinline__ Match lookup_fsm2(const KParams& P, const ProbeL& t, 
       // (after two slots, h1 may be occupied without its record: it is
       // loaded here).
       have2 = false;
-    }
-    if (M == 2 && OO_RX_FSM2_FAM) a6 = __ballot(live && t.is6) != 0;
-    if (live) {
-      occ = probe_occ(P, t, h1);
-      if (occ) {
-        rec = load_rec(P, t, h1, any6 && a6);
-        const uint32_t n = (h1 + h2) & t.mask;
-        have2 = n != first && probe_occ(P, t, n);
-        if (have2) rec2 = load_rec(P, t, n, any6 && a6);
+      if (live) {
+        occ = probe_occ(P, t, h1);
+        if (occ) {
+          rec = load_rec(P, t, h1, any6);
+          const uint32_t n = (h1 + h2) & t.mask;
+          have2 = n != first && probe_occ(P, t, n);
+          if (have2) rec2 = load_rec(P, t, n, any6);
+        }
       }
     }
   }
