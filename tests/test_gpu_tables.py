@@ -230,3 +230,48 @@ def test_more_streams_than_tracked_entries(cuda):
     entry's new stream waits for the old one), with streams given up by
     oo_gpu_rx_stream_done and replaced as they go."""
     _run_streams(cuda, 11, 33, 2, 1 << 16, done_every=5)
+
+
+def test_table_changes_across_destroyed_and_recreated_streams(cuda):
+    """a table flush runs on stream A, the caller gives A up
+    (oo_gpu_rx_stream_done) and destroys it, and a new stream -- often with
+    the same handle -- runs the next batch after another change: that batch
+    must wait for the flush (the context forgets A's handle at stream_done)
+    and see the new tables.  Raw HIP streams (torch pools its own, so its
+    handles never die); no synchronisation between the rounds."""
+    import ctypes
+    torch = cuda
+    # the HIP runtime this process already runs (torch's), never a second copy
+    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+    hip = ctypes.CDLL(path)
+    filters, socks = pktgen.world(2)
+    g = GpuRxStack(device=0)
+    o = OracleStack()
+    for st in (g, o):
+        st.load_world(filters, socks)
+    n = 1 << 14
+    buf, desc = pktgen.generate(2, n, first=5)
+    fr, de = to_dev(buf), to_dev(desc)
+    victims = filters[:8]
+    outs, wants = [], []
+    torch.cuda.synchronize()
+    for r in range(16):
+        f = victims[r % len(victims)]
+        for st in (g, o):  # remove on even rounds, put back on odd ones
+            rc = (st.filter_remove_raw if r % 2 == 0 else st.filter_insert_raw)(*_raw(f))
+            assert rc == 0
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        out = torch.full((n * 32,), 0xAB, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # (the output's fill, on torch's stream)
+        g.handle_rx_batch_dev(fr.data_ptr(), fr.numel(), de.data_ptr(), n, out.data_ptr(), 0,
+                              s.value)
+        g.stream_done(s.value)
+        assert hip.hipStreamDestroy(s) == 0
+        outs.append(out)
+        wants.append(o.handle_rx_batch(buf, desc, nthreads=8))
+    torch.cuda.synchronize()
+    for r, (out, want) in enumerate(zip(outs, wants)):
+        got = out.cpu().numpy().view(_abi.RESULT_DTYPE)
+        assert got.tobytes() == want.tobytes(), f"round {r}: " + diff_report(got, want, desc)
+    g.close()
