@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OO_GPU_RX_ABI_VERSION 3
+#define OO_GPU_RX_ABI_VERSION 4
 
 /* intf_i -> hwport map size (CI_CFG_MAX_INTERFACES = 30,
  * src/include/ci/internal/transport_config_opt.h:29). */
@@ -299,6 +299,9 @@ typedef struct oo_gpu_rx_tuning {
   uint32_t body_engine;    /* body_kernel: 0 by frame size (per-group job
                               sequences for frames under 1 KiB of buffer,
                               else lockstep slots), 1 lockstep, 2 sequences */
+  uint32_t walks;          /* 1: every lookup walks the filter table (no key
+                              index); 0: the key index answers the keys it
+                              holds (DESIGN.md "The key index")              */
 } oo_gpu_rx_tuning;
 int oo_gpu_rx_set_tuning(oo_gpu_rx_ctx* ctx, const oo_gpu_rx_tuning* t);
 

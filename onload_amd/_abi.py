@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboo_gpu_rx.so")
 PKTGEN_PATH = os.path.join(_HERE, "liboo_pktgen.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_INTF = 32
 
 # Reason codes (oo_gpu_rx.h), in the reference's check order.
@@ -76,7 +76,7 @@ class Tuning(ctypes.Structure):
                 ("static_tiles", ctypes.c_uint32), ("tail_tile", ctypes.c_uint32),
                 ("tail_per_wave", ctypes.c_uint32), ("tstep", ctypes.c_uint32),
                 ("body_bpc", ctypes.c_uint32), ("body_tail", ctypes.c_uint32),
-                ("body_engine", ctypes.c_uint32)]
+                ("body_engine", ctypes.c_uint32), ("walks", ctypes.c_uint32)]
 
 
 #: The measurement settings tests and tools pass through the environment of
@@ -85,7 +85,7 @@ TUNING_ENV = {"OO_RX_KERNEL": "path", "OO_RX_GRID_PCT": "grid_pct", "OO_RX_GROUP
               "OO_RX_GSHIFT": "gshift", "OO_RX_STATIC": "static_tiles",
               "OO_RX_TAIL_TILE": "tail_tile", "OO_RX_TAIL_PER_WAVE": "tail_per_wave",
               "OO_RX_TSTEP": "tstep", "OO_RX_BODY_BPC": "body_bpc", "OO_RX_BODY_TAIL": "body_tail",
-              "OO_RX_BODY_ENGINE": "body_engine"}
+              "OO_RX_BODY_ENGINE": "body_engine", "OO_RX_WALKS": "walks"}
 
 
 def tuning_from_env() -> "Tuning | None":

@@ -50,6 +50,9 @@ extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::Table
 extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s);
 extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s);
 extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s);
+extern "C" int oo_table_launch_kx(const oo_rx::DevTables* T, hipStream_t s);
+extern "C" uint64_t oo_table_kx_bytes4(uint32_t nb4);
+extern "C" uint64_t oo_table_kx_bytes6(uint32_t ne6);
 
 namespace {
 
@@ -215,6 +218,7 @@ struct oo_gpu_rx_ctx {
   uint32_t grid_body = 0;      // resident blocks of body_kernel
   uint32_t grid_body_gseq = 0; // ... of its per-group-sequence instance
   uint32_t body_engine = 0;    // oo_gpu_rx_tuning::body_engine
+  bool kx = true;              // lookups through the key index (oo_gpu_rx_tuning::walks)
   uint32_t body_tail = 16;     // packets per body_kernel unit at the batch's end
   uint32_t kmode = 0;          // rx kernel: 0 by frame size, 1 always the 4-slot, 2 always the 2-slot
   uint32_t len_hint = 0;       // mean frame length of the batches to come (0: from buffer bytes)
@@ -536,7 +540,8 @@ void mirror_from_image(oo_gpu_rx_ctx* c, const uint8_t* src) {
 void free_dev(oo_gpu_rx_ctx* c) {
   DevTables& T = c->T;
   for (void* p : {(void*)T.slot4, (void*)T.rc4, (void*)T.occ4, (void*)T.slot6, (void*)T.occ6,
-                  (void*)T.socks, (void*)T.sockgen, (void*)c->d_zero, (void*)c->d_claim})
+                  (void*)T.socks, (void*)T.sockgen, (void*)c->d_zero, (void*)c->d_claim,
+                  (void*)T.kx4, (void*)T.kx6, (void*)T.kx_ok})
     if (p) (void)hipFree(p);
   for (OpStage& st : c->stage) {
     if (st.h) (void)hipHostFree(st.h);
@@ -665,7 +670,8 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
     }
     st.pending = true;
   }
-  if (c->ops_sock && oo_table_launch_refresh(&c->T, c->gen, s) != 0) {
+  if ((c->ops_sock && oo_table_launch_refresh(&c->T, c->gen, s) != 0) ||
+      oo_table_launch_kx(&c->T, s) != 0) {
     c->failed = true;
     return -EIO;
   }
@@ -746,6 +752,7 @@ void apply_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
   c->grid_body = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]);
   c->grid_body_gseq = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[4]) : c->bpc[4]);
   c->body_engine = t->body_engine;
+  c->kx = t->walks == 0;
   c->kmode = t->path;
   c->tstep = t->tstep == 1 ? 1 : 8;
   c->dyn = t->static_tiles == 0;
@@ -763,7 +770,8 @@ extern "C" {
 int oo_gpu_rx_abi_version(void) { return OO_GPU_RX_ABI_VERSION; }
 
 int oo_gpu_rx_set_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
-  if (c == nullptr || (t != nullptr && (t->path > 3 || t->grid_pct > 100 || t->body_engine > 2))) return -EINVAL;
+  if (c == nullptr || (t != nullptr && (t->path > 3 || t->grid_pct > 100 || t->body_engine > 2 ||
+                                  t->walks > 1))) return -EINVAL;
   apply_tuning(c, t);
   return 0;
 }
@@ -821,6 +829,10 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   T.ip6_mask = c->ip6_mask;
   T.max_socks = c->max_socks;
   const uint64_t n4 = c->ip4_mask + 1ull, n6 = c->ip6_mask + 1ull;
+  // The key index: per protocol up to 2^17 buckets of two entries, up to
+  // 2^17 IPv6 entries (a table with more keys than that turns it off).
+  T.kx_nb4 = (uint32_t)std::min<uint64_t>(n4, 1u << 17);
+  T.kx_ne6 = (uint32_t)std::min<uint64_t>(4 * n6, 1u << 17);
   bool ok =
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
       hipEventCreateWithFlags(&c->tables_ev, hipEventDisableTiming) == hipSuccess &&
@@ -839,7 +851,10 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
       hipMemsetAsync(c->d_zero, 0, 16u * oo_rx::ZERO_LINES, c->stream) == hipSuccess &&
       hipMemcpyAsync(c->d_zero + 16u * oo_rx::ZERO_LINES + oo_rx::SINK_BYTES, c->hwport,
                      OO_GPU_RX_MAX_INTF, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
-      oo_table_launch_init(&T, c->stream) == 0;
+      oo_table_launch_init(&T, c->stream) == 0 &&
+      hipMalloc(&T.kx4, oo_table_kx_bytes4(T.kx_nb4)) == hipSuccess &&
+      hipMalloc(&T.kx6, oo_table_kx_bytes6(T.kx_ne6)) == hipSuccess &&
+      hipMalloc(&T.kx_ok, 128) == hipSuccess && oo_table_launch_kx(&T, c->stream) == 0;
   for (OpStage& st : c->stage)
     ok = ok && hipHostMalloc(&st.h, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK,
                              hipHostMallocDefault) == hipSuccess &&
@@ -1057,7 +1072,7 @@ int oo_gpu_rx_table_import(oo_gpu_rx_ctx* c, const void* src, uint64_t bytes, vo
           hipSuccess &&
       hipMemcpyAsync(c->T.socks, d + h.off_socks, sizeof(oo_gpu_rx_sock) * c->max_socks,
                      hipMemcpyDefault, s) == hipSuccess &&
-      oo_table_launch_occ(&c->T, s) == 0;
+      oo_table_launch_occ(&c->T, s) == 0 && oo_table_launch_kx(&c->T, s) == 0;
   // From here on the mirror holds the image: a failure leaves the device
   // copy unknown.
   Tracked* t = ok ? track_of(c, s) : nullptr;
@@ -1179,6 +1194,13 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   P.occ4 = c->T.occ4;
   P.slot6 = c->T.slot6;
   P.occ6 = c->T.occ6;
+  if (c->kx) {
+    P.kx4 = c->T.kx4;
+    P.kx6 = c->T.kx6;
+    P.kx_ok = c->T.kx_ok;
+    P.kx_nb4 = c->T.kx_nb4;
+    P.kx_ne6 = c->T.kx_ne6;
+  }
   P.zero = c->d_zero;
   P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
   P.stamps = c->stamps;

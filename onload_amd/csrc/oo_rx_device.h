@@ -122,6 +122,43 @@ struct TableOp {
 };
 static_assert(sizeof(TableOp) == 64, "table op layout");
 
+// The key index (DESIGN.md "The key index"): the answer of every lookup key
+// that has one, rebuilt on the device after each table change
+// (oo_table_kernel.hip table_kx).  A lookup is then one load level instead
+// of a walk along Onload's probe sequence.  Keys are a stage's lookup tuple;
+// the value is the socket id of the walk's first match, with KX_FB when the
+// walk's answer depends on the packet (a bind2dev socket among the matches)
+// or its match count is not 1 (UDP) -- those lanes walk the table.
+//  IPv4: two regions (UDP, then TCP) of kx_nb4 + KX_PAD4 buckets, a bucket
+//   two 16-B entries {laddr, raddr, lport | rport << 16, value}.
+//  IPv6: kx_ne6 + KX_PAD6 entries of 64 B {laddr[4], raddr[4],
+//   lport | rport << 16, proto | wildcard << 8, value, 0 x 5}; a wildcard key
+//   (raddr and rport zero) is a lookup with ra_null: unconnected sockets.
+// A key is placed at its hash's bucket (entry) or the first free one after
+// it, never wrapping: the last KX_OVF are overflow room, the pad after them
+// always empty (a two-bucket load at the end reads it).  Value 0: empty.
+constexpr uint32_t KX_VALID = 0x80000000u;
+constexpr uint32_t KX_FB = 0x40000000u;
+constexpr uint32_t KX_OVF = 64;
+constexpr uint32_t KX_PAD4 = KX_OVF + 2, KX_PAD6 = KX_OVF + 1;
+constexpr uint32_t KX_WALK_MAX = 4096;  // a longer build walk turns the index off
+
+OO_HD uint32_t kx_mix(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x7feb352du;
+  h ^= h >> 15;
+  h *= 0x846ca68bu;
+  h ^= h >> 16;
+  return h;
+}
+// The key hash: IPv4 keys with la[1..3] = ra[1..3] = 0 and pw = 0.
+OO_HD uint32_t kx_hash(uint32_t la0, uint32_t la1, uint32_t la2, uint32_t la3, uint32_t ra0,
+                       uint32_t ra1, uint32_t ra2, uint32_t ra3, uint32_t ports, uint32_t pw) {
+  return kx_mix(la0 * 0x9e3779b1u + la1 * 0x85ebca77u + la2 * 0xc2b2ae3du + la3 * 0x27d4eb2fu +
+                ra0 * 0x165667b1u + ra1 * 0xd3a2646du + ra2 * 0xfd7046c5u + ra3 * 0xb55a4f09u +
+                ports * 0x2545f491u + pw * 0x9e3779b9u);
+}
+
 // Device-resident filter-table state of a context.
 struct DevTables {
   Slot4* slot4;
@@ -132,6 +169,12 @@ struct DevTables {
   oo_gpu_rx_sock* socks;
   uint32_t* sockgen;  // flush generation of each socket's last change
   uint32_t ip4_mask, ip6_mask, max_socks;
+  // The key index (null: none).
+  uint32_t* kx4;
+  uint32_t* kx6;
+  uint32_t* kx_ok;    // 1: the index answers lookups (0: walks only)
+  uint32_t kx_nb4;    // main IPv4 buckets per protocol region (a power of two)
+  uint32_t kx_ne6;    // main IPv6 entries (a power of two)
 };
 
 // The zero region read by lanes that have no chunk to load (64 KiB, so
@@ -202,6 +245,11 @@ struct KParams {
   const uint8_t* hwport;  // intf_i_to_hwport, OO_GPU_RX_MAX_INTF bytes in device memory
   uint64_t* pend;        // split transform: a pending word per packet (n + 64 entries)
   uint32_t* flag;        // split transform: non-zero once a verdict waits for a body
+  // The key index (DevTables kx*); kx4 null: lookups walk the tables.
+  const uint32_t* kx4;
+  const uint32_t* kx6;
+  const uint32_t* kx_ok;
+  uint32_t kx_nb4, kx_ne6;
 };
 
 }  // namespace oo_rx

@@ -1259,6 +1259,138 @@ __device__ __forceinline__ Match lookup_fsm2(const KParams& P, const ProbeL& t, 
   return m;
 }
 
+// The lookups through the key index (oo_rx_device.h; DESIGN.md "The key
+// index"): every stage's key of the lane in one load level -- a 32-B bucket
+// (IPv4; 48 B, with the next bucket's first entry, in a wave that also holds
+// IPv6 lanes) or the first 48 B of a 64-B entry (IPv6) per key -- and another
+// level only for a key whose bucket was full.  The index's flag word comes with them (a scalar load: no vector
+// wait of its own).  Returns true for a lane whose m / stage / s2 it set as
+// the walks would have; false for a lane that must walk: an answer that
+// depends on the packet's interface or VLAN (bind2dev), a UDP key with
+// other than one match, or an index the last table change turned off.
+template <bool ANY6>
+__device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool look, bool tcp,
+                                          bool any_tcp, uint32_t dport, uint32_t sport,
+                                          uint32_t proto, bool o0, bool o1, bool o2, Match& m,
+                                          int& stage, bool& s2) {
+  const bool six = ANY6 && h.is6;
+  uint32_t la[4], sa[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    la[i] = i == 0 || six ? h.da[i] : 0u;
+    sa[i] = i == 0 || six ? h.sa[i] : 0u;
+  }
+  const uint32_t p0 = dport | (sport << 16);
+  const uint32_t pw0 = six ? proto : 0u, pw1 = six ? proto | 0x100u : 0u;
+  uint32_t pos[3];
+  pos[0] = kx_hash(la[0], la[1], la[2], la[3], sa[0], sa[1], sa[2], sa[3], p0, pw0);
+  pos[1] = kx_hash(la[0], la[1], la[2], la[3], 0u, 0u, 0u, 0u, dport, pw1);
+  pos[2] = kx_hash(0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, dport, pw1);
+  const uint32_t pmask = six ? sreg(P.kx_ne6) - 1u : sreg(P.kx_nb4) - 1u;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pos[k] &= pmask;
+  const uint64_t b4 = sreg64(P.kx4), b6 = sreg64(P.kx6);
+  const uint64_t t4 = b4 + (uint64_t)(sreg(P.kx_nb4) + KX_PAD4) * 32u;
+  const uint64_t base = six ? b6 : (tcp ? t4 : b4);
+  const uint32_t shift = six ? 6u : 5u;
+  const int nk = any_tcp ? 3 : 2;
+  uint32_t okw;
+  {
+    const uint64_t fa = sreg64(P.kx_ok);
+    asm volatile("s_load_dword %0, %1, 0x0" : "=s"(okw) : "s"(fa));
+  }
+  uint32_t val[3] = {0u, 0u, 0u};
+  // Only keys whose first table slot is occupied: any other walk ends at
+  // once without a match (its key is not in the index either).
+  bool pend[3] = {look && o0, look && o1, look && tcp && o2};
+  // One level: every pending key's bucket (entry) loaded, then compared.
+  auto level = [&]() __attribute__((always_inline)) {
+    uint4 d[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k < nk) {
+        // (a key not looked up reads the region's first bucket: one line
+        // for the wave, no branch around the batch)
+        const uint64_t a = base + ((uint64_t)(pend[k] ? pos[k] : 0u) << shift);
+        d[k][0] = gload16(a);
+        d[k][1] = gload16(a + 16u);
+        if (ANY6) d[k][2] = gload16(a + 32u);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k < nk && pend[k]) {
+        const uint32_t kra = k == 0 ? sa[0] : 0u, kp = k == 0 ? p0 : dport;
+        const uint32_t kla = k == 2 ? 0u : la[0];
+        uint32_t hv = 0u;
+        bool empty = false;
+#pragma unroll
+        for (int j = 0; j < (ANY6 ? 3 : 2); ++j) {
+          const uint4 e = d[k][j];
+          const bool hj = (e.w != 0u) & (e.x == kla) & (e.y == kra) & (e.z == kp);
+          hv = hj ? e.w : hv;
+          empty |= e.w == 0u;
+        }
+        if (ANY6 && six) {
+          bool eq = (d[k][2].z != 0u) & (d[k][2].x == kp) & (d[k][2].y == (k == 0 ? pw0 : pw1));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t ei = i == 0 ? d[k][0].x : i == 1 ? d[k][0].y : i == 2 ? d[k][0].z : d[k][0].w;
+            const uint32_t ri = i == 0 ? d[k][1].x : i == 1 ? d[k][1].y : i == 2 ? d[k][1].z : d[k][1].w;
+            eq = eq & (ei == (k == 2 ? 0u : la[i])) & (ri == (k == 0 ? sa[i] : 0u));
+          }
+          hv = eq ? d[k][2].z : 0u;
+          empty = d[k][2].z == 0u;
+        }
+        if (hv != 0u) {
+          val[k] = hv;
+          pend[k] = false;
+        } else if (empty) {
+          pend[k] = false;
+        } else {
+          pos[k] += 1u;
+        }
+      }
+    }
+  };
+  // The first level is issued at once (a loop head would first wait for
+  // every load in flight, the body stream's included); the loop takes the
+  // rare keys whose bucket was full.
+  level();
+  bool left = false;
+  for (uint32_t it = 1;; ++it) {
+    const bool any = pend[0] || pend[1] || pend[2];
+    if (__ballot(any) == 0) break;
+    if (it > KX_OVF + 2u) {  // (cannot happen: a pad bucket is always empty)
+      left = any;
+      break;
+    }
+    level();
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(okw));
+  const bool f0 = val[0] != 0u, f1 = val[1] != 0u, f2 = tcp && val[2] != 0u;
+  bool fb = left;
+  uint32_t v = 0u;
+  if (f0) {
+    v = val[0];
+    stage = 1;
+    if (!tcp && !six) {  // IPv4 UDP: stage 2 for the future rule (lookup_stages)
+      s2 = f1;
+      fb = fb || (f1 && (val[1] & KX_FB) != 0u);
+    }
+  } else if (f1) {
+    v = val[1];
+    stage = 2;
+  } else if (f2) {
+    v = val[2];
+    stage = 3;
+  }
+  fb = fb || (v & KX_FB) != 0u || okw == 0u;
+  m.first = v != 0u ? (int32_t)(v & ID_MASK) : -1;
+  m.n = v != 0u ? 1u : 0u;
+  return look && !fb;
+}
+
 // The record of one packet from its headers: the lookup stages of
 // ci_udp_handle_rx (udp_rx.c:271-306: full 4-tuple, then (laddr, lport)) or
 // ci_tcp_handle_rx (tcp_rx.c:4786-4835: then (*, lport)); the first stage
@@ -1346,9 +1478,15 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     // and that record usually decides); a later stage loads its own only
     // when this one did not match.
     const int fs = o0 ? 0 : o1 ? 1 : o2 ? 2 : 3;
+    // Lanes that walk the tables: all that look up, less those the key
+    // index answers.
+    bool walkl = look;
+    if (P.kx4 != nullptr)
+      walkl = look && !kx_lookup<ANY6>(P, h, look, tcp, any_tcp, dport, sport, proto, o0, o1, o2, m,
+                                       stage, s2);
     Rec rec = {};
-    if (look && fs < 3) rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
-    if (look) {
+    if (walkl && fs < 3) rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
+    if (walkl) {
       DSTAMP(9);
       // Both families walk in one instruction stream (lookup_stages<2>).
       // Waves with TCP lookups (three stages, long connected-socket chains)

@@ -308,6 +308,177 @@ __global__ __launch_bounds__(256) void table_occ(DevTables T) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The key index (oo_rx_device.h): one thread per slot.  A slot whose entry is
+// the first match of its own key's walk -- the walk the RX kernels would do
+// for a packet of that key, netif_table.c:234-319 / netif_table_ip6.c:110-189
+// -- puts the key's answer into the index; every other key has no match, and
+// finds no entry.  Keys are exact tuples: on IPv4 the first probe's unchecked
+// lport is safe by the Local Port Recovery Property of tables of 2^16+ slots
+// (netif_table.c:276-290), for entries at the slot their key hashes to; an
+// entry left PREFERRED elsewhere (its socket's fields changed after the
+// insert) turns the index off, as do a full overflow room and a walk longer
+// than KX_WALK_MAX.
+
+__device__ __forceinline__ void kx_off(const DevTables& T) { T.kx_ok[0] = 0u; }
+
+struct KxWalk {
+  uint32_t first;  // slot of the first match (~0u: none)
+  uint32_t n;      // matches (TCP: stops at the first)
+  bool b2d;        // a match is a bind2dev socket (its verdict depends on the packet)
+  bool ok;         // false: walk too long
+};
+
+__device__ KxWalk kx_walk4(const DevTables& T, uint32_t la, uint32_t lp, uint32_t ra, uint32_t rp,
+                           uint32_t proto) {
+  KxWalk w = {~0u, 0u, false, true};
+  const uint32_t first = hash3(la, lp, ra, rp, proto) & T.ip4_mask;
+  const uint32_t h2 = hash2(la, lp, ra, rp, proto);
+  uint32_t k = first;
+  Slot4 e = T.slot4[k];
+  auto hit = [&](uint32_t at, const Slot4& s) {
+    if (w.n == 0) w.first = at;
+    ++w.n;
+    w.b2d |= (s.sflags & OO_GPU_RX_SOCK_BIND2DEV) != 0;
+  };
+  // the first probe: a PREFERRED entry, lport implied (netif_table.c:291-297)
+  if ((e.id_state & ST_MASK) == ST_PREFERRED && e.laddr == la && e.raddr == ra && e.rport == rp &&
+      e.proto == proto)
+    hit(k, e);
+  for (uint32_t steps = 0; !(proto == 6u && w.n != 0); ++steps) {
+    if ((e.id_state & ST_MASK) == ST_EMPTY) break;
+    k = (k + h2) & T.ip4_mask;
+    if (k == first) break;
+    if (steps >= KX_WALK_MAX) {
+      w.ok = false;
+      break;
+    }
+    e = T.slot4[k];
+    if (occupied(e.id_state) && e.laddr == la && e.lport == lp && e.raddr == ra && e.rport == rp &&
+        e.proto == proto)
+      hit(k, e);
+  }
+  return w;
+}
+
+__device__ KxWalk kx_walk6(const DevTables& T, const uint32_t la[4], uint32_t lp,
+                           const uint32_t ra[4], uint32_t rp, uint32_t proto, bool wild) {
+  KxWalk w = {~0u, 0u, false, true};
+  const uint32_t lx = addr_xor4(la), rx = wild ? 0u : addr_xor4(ra);
+  const uint32_t first = hash3(lx, lp, rx, wild ? 0u : rp, proto) & T.ip6_mask;
+  const uint32_t h2 = hash2(lx, lp, rx, wild ? 0u : rp, proto);
+  uint32_t k = first;
+  for (uint32_t steps = 0;; ++steps) {
+    const Slot6 e = T.slot6[k];
+    if (e.id == ID6_EMPTY) break;
+    const bool rok = wild ? !(e.sflags & OO_GPU_RX_SOCK_CONNECTED)
+                          : (e.raddr[0] == ra[0] && e.raddr[1] == ra[1] && e.raddr[2] == ra[2] &&
+                             e.raddr[3] == ra[3] && e.rport == rp);
+    if (e.id >= 0 && laddr6_eq(e, la) && e.lport == lp && e.proto == proto && rok) {
+      if (w.n == 0) w.first = k;
+      ++w.n;
+      w.b2d |= (e.sflags & OO_GPU_RX_SOCK_BIND2DEV) != 0;
+      if (proto == 6u) break;  // TCP: the first match ends the walk
+    }
+    k = (k + h2) & T.ip6_mask;
+    if (k == first) break;
+    if (steps >= KX_WALK_MAX) {
+      w.ok = false;
+      break;
+    }
+  }
+  return w;
+}
+
+__device__ __forceinline__ uint32_t kx_value(const KxWalk& w, uint32_t id, uint32_t proto) {
+  const bool fb = w.b2d || (proto == 17u && w.n != 1u);
+  return KX_VALID | (fb ? KX_FB : 0u) | (id & ID_MASK);
+}
+
+// Claims the first free entry at or after the key's bucket (two entries of
+// 16 B per bucket); false when the overflow room is full.
+__device__ bool kx_put4(const DevTables& T, uint32_t proto, uint32_t la, uint32_t ra, uint32_t ports,
+                        uint32_t val) {
+  uint32_t* base = T.kx4 + (proto == 6u ? (size_t)(T.kx_nb4 + KX_PAD4) * 8u : 0u);
+  const uint32_t b = kx_hash(la, 0, 0, 0, ra, 0, 0, 0, ports, 0) & (T.kx_nb4 - 1u);
+  for (uint32_t q = b; q < T.kx_nb4 + KX_OVF; ++q) {
+    for (uint32_t e = 0; e < 2; ++e) {
+      uint32_t* ent = base + (size_t)q * 8u + e * 4u;
+      if (atomicCAS(ent + 3, 0u, val) == 0u) {
+        ent[0] = la;
+        ent[1] = ra;
+        ent[2] = ports;
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
+__device__ bool kx_put6(const DevTables& T, const uint32_t la[4], const uint32_t ra[4],
+                        uint32_t ports, uint32_t pw, uint32_t val) {
+  const uint32_t b = kx_hash(la[0], la[1], la[2], la[3], ra[0], ra[1], ra[2], ra[3], ports, pw) &
+                     (T.kx_ne6 - 1u);
+  for (uint32_t q = b; q < T.kx_ne6 + KX_OVF; ++q) {
+    uint32_t* ent = T.kx6 + (size_t)q * 16u;
+    if (atomicCAS(ent + 10, 0u, val) == 0u) {
+      for (int i = 0; i < 4; ++i) {
+        ent[i] = la[i];
+        ent[4 + i] = ra[i];
+      }
+      ent[8] = ports;
+      ent[9] = pw;
+      return true;
+    }
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void table_kx(DevTables T) {
+  const uint32_t n4 = T.ip4_mask + 1u, n6 = T.ip6_mask + 1u;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4 + n6;
+       i += gridDim.x * blockDim.x) {
+    if (i < n4) {
+      const Slot4 r = T.slot4[i];
+      const uint32_t st = r.id_state;
+      const uint32_t id = st & ID_MASK;
+      if (!occupied(st) || id >= T.max_socks || (r.proto != 6u && r.proto != 17u)) continue;
+      if ((st & ST_MASK) == ST_PREFERRED &&
+          (hash3(r.laddr, r.lport, r.raddr, r.rport, r.proto) & T.ip4_mask) != i) {
+        kx_off(T);
+        continue;
+      }
+      const KxWalk w = kx_walk4(T, r.laddr, r.lport, r.raddr, r.rport, r.proto);
+      if (!w.ok) {
+        kx_off(T);
+      } else if (w.first == i &&
+                 !kx_put4(T, r.proto, r.laddr, r.raddr, (uint32_t)r.lport | ((uint32_t)r.rport << 16),
+                          kx_value(w, id, r.proto))) {
+        kx_off(T);
+      }
+    } else {
+      const uint32_t j = i - n4;
+      const Slot6 r = T.slot6[j];
+      if (r.id < 0 || (uint32_t)r.id >= T.max_socks || (r.proto != 6u && r.proto != 17u)) continue;
+      const uint32_t zero[4] = {0, 0, 0, 0};
+      // the exact tuple (stage 1), and for an unconnected socket the
+      // wildcard (stages 2 and 3, ra_null)
+      for (int wild = 0; wild < 2; ++wild) {
+        if (wild && (r.sflags & OO_GPU_RX_SOCK_CONNECTED)) break;
+        const KxWalk w = kx_walk6(T, r.laddr, r.lport, r.raddr, r.rport, r.proto, wild != 0);
+        if (!w.ok) {
+          kx_off(T);
+        } else if (w.first == j &&
+                   !kx_put6(T, r.laddr, wild ? zero : r.raddr,
+                            (uint32_t)r.lport | (wild ? 0u : (uint32_t)r.rport << 16),
+                            r.proto | (wild ? 0x100u : 0u), kx_value(w, (uint32_t)r.id, r.proto))) {
+          kx_off(T);
+        }
+      }
+    }
+  }
+}
+
 }  // namespace oo_rx
 
 namespace {
@@ -335,6 +506,27 @@ extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s) {
   hipLaunchKernelGGL(oo_rx::table_init,
                      dim3(grid_for(T->ip4_mask + T->ip6_mask + 2u + T->max_socks)), dim3(256), 0,
                      s, *T);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Bytes of the two index arrays (oo_rx_device.h).
+extern "C" uint64_t oo_table_kx_bytes4(uint32_t nb4) {
+  return 2ull * (nb4 + oo_rx::KX_PAD4) * 32u;
+}
+extern "C" uint64_t oo_table_kx_bytes6(uint32_t ne6) {
+  return (uint64_t)(ne6 + oo_rx::KX_PAD6) * 64u;
+}
+
+// The key index from the current tables, on s after the change that made
+// them: cleared, marked usable, rebuilt (each check that fails marks it off).
+extern "C" int oo_table_launch_kx(const oo_rx::DevTables* T, hipStream_t s) {
+  if (T->kx4 == nullptr) return 0;
+  if (hipMemsetAsync(T->kx4, 0, oo_table_kx_bytes4(T->kx_nb4), s) != hipSuccess ||
+      hipMemsetAsync(T->kx6, 0, oo_table_kx_bytes6(T->kx_ne6), s) != hipSuccess ||
+      hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(T->kx_ok), 1, 1, s) != hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(oo_rx::table_kx, dim3(grid_for(T->ip4_mask + T->ip6_mask + 2u)), dim3(256), 0, s,
+                     *T);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -24,7 +24,9 @@ def test_tuning_validated():
         g.set_tuning(_tuning(path=path))
     for engine in (0, 1, 2):
         g.set_tuning(_tuning(path=3, body_engine=engine))
-    for bad in (dict(path=4), dict(grid_pct=101), dict(body_engine=3)):
+    for walks in (0, 1):
+        g.set_tuning(_tuning(walks=walks))
+    for bad in (dict(path=4), dict(grid_pct=101), dict(body_engine=3), dict(walks=2)):
         with pytest.raises(OSError):
             g.set_tuning(_tuning(**bad))
     g.close()
