@@ -2905,6 +2905,9 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
 
 __global__ __launch_bounds__(WAVES_W * 64) __attribute__((amdgpu_waves_per_eu(OO_RX_WIN_WPE))) void win_kernel(
     KParams P) {
+#ifdef OO_RX_STAMPS
+  dstamp_slot(nullptr, true);  // (no phase stamps from this kernel's demux)
+#endif
   window_loop(P);
 }
 #endif  // !OO_RX_SHORT

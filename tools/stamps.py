@@ -41,6 +41,9 @@ def main() -> None:
     from onload_amd import pktgen
     from onload_amd.rx import GpuRxStack
 
+    # The stamps come from rx_kernel's tile loop: its instance for the
+    # configuration (the split transform's kernels write none).
+    os.environ.setdefault("OO_RX_KERNEL", "2" if args.config in (3, 5) else "1")
     dev = torch.device("cuda", 0)
     n = args.n or DEFAULT_N[args.config]
     filters, socks = pktgen.world(args.config)
