@@ -103,6 +103,15 @@ struct Entry6 {
 static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
               "entry layouts");
 
+#ifndef OO_KX_LOG2_MAX
+#define OO_KX_LOG2_MAX 17  // key index: buckets per IPv4 region / IPv6 entries at most, log2
+#endif
+#ifndef OO_KX_V4_MUL
+#define OO_KX_V4_MUL 1  // IPv4 buckets per protocol region per table slot
+#endif
+#ifndef OO_KX_V6_MUL
+#define OO_KX_V6_MUL 4  // IPv6 index entries per table slot
+#endif
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
 constexpr int NTRACK = 8;             // streams tracked at once (LRU)
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
@@ -831,8 +840,8 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   const uint64_t n4 = c->ip4_mask + 1ull, n6 = c->ip6_mask + 1ull;
   // The key index: per protocol up to 2^17 buckets of two entries, up to
   // 2^17 IPv6 entries (a table with more keys than that turns it off).
-  T.kx_nb4 = (uint32_t)std::min<uint64_t>(n4, 1u << 17);
-  T.kx_ne6 = (uint32_t)std::min<uint64_t>(4 * n6, 1u << 17);
+  T.kx_nb4 = (uint32_t)std::min<uint64_t>(OO_KX_V4_MUL * n4, 1u << OO_KX_LOG2_MAX);
+  T.kx_ne6 = (uint32_t)std::min<uint64_t>(OO_KX_V6_MUL * n6, 1u << OO_KX_LOG2_MAX);
   bool ok =
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
       hipEventCreateWithFlags(&c->tables_ev, hipEventDisableTiming) == hipSuccess &&
