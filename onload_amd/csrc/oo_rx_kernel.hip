@@ -2543,7 +2543,10 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     STAMP(1, __builtin_amdgcn_s_memrealtime());
     STAMP(7, T0);
 
-    // Rounds R..R+E-1 into the header rows, once their windows are read.
+    // Rounds R..R+E-1 into the header rows, once their windows are read --
+    // and after the demux: issued before it they are older than its loads,
+    // and every demux wait would wait for them too (configs 2/4/5 -1.7 /
+    // -0.5 / -0.7 %, profiles/r04/ab_extra_after_demux.log).
     auto issue_extra = [&]() {
       if (ext) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2560,7 +2563,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       issue_extra();
     } else {
       const Hdr h = parse_headers(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
-      issue_extra();
       STAMP(2, __builtin_amdgcn_s_memrealtime());
 #ifdef OO_RX_STAMPS
       if (lane == 0)
@@ -2568,6 +2570,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
                     true);
 #endif
       ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
+      issue_extra();
     }
     STAMP(3, __builtin_amdgcn_s_memrealtime());
 
@@ -2850,6 +2853,10 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     uint32_t wl = lane;
     asm volatile("" : "+v"(wl));
     const Hdr h = parse_headers(window_of(L.hdr, wl), dv.shift, dv.len, dv.abase);
+    // ---- lookups and the record: before the next tile's staging, so the
+    // demux's waits do not also wait for those loads (config 3 -0.3 to -2 %,
+    // profiles/r04/ab_win_demux_first.log).
+    Parsed ps = demux_packet<true>(P, h, dv.intf_i, dv.abase, dv.span, dv.shift, lds_occ);
 
     // ---- stage the next tile: its windows into the rows the parse has
     // read (its descriptor line: newer are the claim and the record stores),
@@ -2876,8 +2883,6 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
     claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
 
-    // ---- lookups and the record.
-    Parsed ps = demux_packet<true>(P, h, dv.intf_i, dv.abase, dv.span, dv.shift, lds_occ);
     const uint32_t reason = ps.r.reason;
     store_records(P, tile, ps.r, lane);
     // The pending words of a tile holding frames with a body.
