@@ -94,6 +94,10 @@ def parse_args(argv=None):
     ap.add_argument("--table-ops", action="store_true",
                     help="also time device-side table maintenance: the world load's flush, "
                          "and a 100-op filter churn batch in front of one batch")
+    ap.add_argument("--group", action="store_true",
+                    help="N=1: run the rank through the library's joined group anyway (a group "
+                         "of one rank: its table image, record gather and counter sum go "
+                         "through librccl); N>1 always does")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-memory path: oo_gpu_rx_submit/_wait, pinned "
                          "double-buffered H2D + transform + D2H")
@@ -212,7 +216,7 @@ def run_rank(args) -> None:
     table_bcast = None
     group = None
     group_path = None
-    if world > 1:
+    if world > 1 or args.group:
         # The library's multi-GPU group across processes (include/oo_gpu_rx.h
         # "Multi-GPU group"): rank 0 makes the RCCL id, torch.distributed's
         # control plane hands it out, every rank joins with one member on its
@@ -220,23 +224,29 @@ def run_rank(args) -> None:
         # table image over RCCL.  Where the join is refused (RCCL takes one
         # rank per GPU: the shared-GPU rehearsal) the Python path over
         # torch.distributed does the same, and the line says which ran.
+        # --group at N=1: a group of one rank, the same librccl calls.
         from onload_amd.group import GpuRxGroup
         gid = [GpuRxGroup.rccl_id() if rank == 0 else None]
-        dist.broadcast_object_list(gid, src=0)
+        if world > 1:
+            dist.broadcast_object_list(gid, src=0)
         try:
             group = GpuRxGroup.join(local, rank, world, gid[0])
         except OSError as e:
+            if world == 1:
+                raise
             log(f"[rank {rank}] group join refused ({e}); torch.distributed path")
-        ok = torch.tensor([1 if group is not None else 0], device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0 and group is not None:
-            group.close()
-            group = None
+        if world > 1:
+            ok = torch.tensor([1 if group is not None else 0], device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and group is not None:
+                group.close()
+                group = None
         group_path = "c_group_rccl" if group is not None else "torch_distributed"
         stack = group.members[0] if group is not None else GpuRxStack(device=local)
         if rank == 0:
             (group or stack).load_world(filters, socks)
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         tb = time.perf_counter()
         if group is not None:
             group.share_tables(sh)
@@ -315,14 +325,17 @@ def run_rank(args) -> None:
                               out.data_ptr(), ctr.data_ptr(), sh)
     torch.cuda.synchronize(dev)
     gather = None
-    if world > 1:
+    if group is not None or world > 1:
         tg = time.perf_counter()
         if group is not None:
             group.sum_counters(ctr.data_ptr(), sh)
-            cnts = torch.tensor([n], dtype=torch.int64, device=dev)
-            allc = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-            dist.all_gather(allc, cnts)
-            counts_r = [int(c.item()) for c in allc]
+            if world > 1:
+                cnts = torch.tensor([n], dtype=torch.int64, device=dev)
+                allc = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+                dist.all_gather(allc, cnts)
+                counts_r = [int(c.item()) for c in allc]
+            else:
+                counts_r = [n]
             recs = (torch.empty(sum(counts_r) * RESULT_B, dtype=torch.uint8, device=dev)
                     if rank == 0 else None)
             group.gather_rccl(out.data_ptr(), n, recs.data_ptr() if rank == 0 else 0,
@@ -336,6 +349,8 @@ def run_rank(args) -> None:
             ok = bool((np.bincount(r, minlength=32) == ctr.cpu().numpy()).all())
             gather = {"records": int(len(r)), "ms": round((time.perf_counter() - tg) * 1e3, 3),
                       "counts_match": ok, "path": group_path}
+            if world == 1:  # a group of one: the records came back through librccl
+                gather["records_equal"] = bool(torch.equal(recs, out[: n * RESULT_B]))
     counts = ctr.cpu().numpy()
     assert counts.sum() == n_total, counts
     path = stack.last_path()  # which kernels the timed launches ran
@@ -427,13 +442,15 @@ def run_rank(args) -> None:
             "cpu_baseline": cpu,
             "hip_env": {"HIP_FORCE_DEV_KERNARG": os.environ.get("HIP_FORCE_DEV_KERNARG")},
             "outcomes": {k: int(v) for k, v in enumerate(counts) if v},
+            "path": group_path or "stack",
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
-        if group is not None:
-            group.close()
+    if group is not None:
+        group.close()
+    if world > 1:
         dist.destroy_process_group()
 
 

@@ -487,15 +487,23 @@ int oo_gpu_rx_group_gather(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards,
                            oo_gpu_rx_result* dst, oo_gpu_rx_counters* counters);
 /* Across processes (every rank calls each, collectively): rank 0's tables
  * to every rank (one image broadcast); rank 0's changes since then, applied
- * by the others in order (returns how many); every rank's n records to
- * rank 0's d_dst in rank order (rank 0 passes counts[nranks]); the device
- * counters summed on every rank. */
+ * by the others in order (returns how many; -EIO on every rank when a
+ * replica's return code differs from rank 0's or rank 0 lost a change, and
+ * the caller then shares the tables again); every rank's n records to
+ * rank 0's d_dst in rank order (rank 0 passes counts[nranks], counts[0] ==
+ * its own n); the device counters summed on every rank.  Each call enters
+ * all of its collectives on every rank and reports a local failure after
+ * them (the staging they use is allocated at the join).  A joined group of
+ * one rank runs the same RCCL calls. */
 int oo_gpu_rx_group_share_tables(oo_gpu_rx_group* g, void* stream);
 int oo_gpu_rx_group_share_ops(oo_gpu_rx_group* g, void* stream);
 int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_out, uint32_t n,
                                 oo_gpu_rx_result* d_dst, const uint32_t* counts, void* stream);
 int oo_gpu_rx_group_sum_counters(oo_gpu_rx_group* g, oo_gpu_rx_counters* d_counters,
                                  void* stream);
+/* 1 when the group's collectives run over RCCL (a joined group, any number
+ * of ranks), 0 for a group opened in one process. */
+int oo_gpu_rx_group_uses_rccl(const oo_gpu_rx_group* g);
 
 /* ---------------------------------------------------------------------
  * Host-pure checksum verifiers: the reference's public C API for this path

@@ -176,6 +176,8 @@ struct ci_netif_gpu_rx {
   uint8_t* handback;
 };
 
+void ci_netif_rx_gpu_close(struct ci_netif_gpu_rx* g);
+
 /* At stack creation, next to ci_netif_filter_init (netif_init.c:105-108).
  * umem: the AF_XDP UMEM the RX ring's addresses index (chunk 2048,
  * tcp_helper_resource.c:2205-2208; efxdp_vi.c:337-348).  The shim reads
@@ -196,8 +198,10 @@ int ci_netif_rx_gpu_open(ci_netif* ni, struct ci_netif_gpu_rx* g, int device,
   g->q = calloc(g->cap, sizeof(*g->q));
   g->orig = calloc(g->cap, sizeof(*g->orig));
   g->handback = calloc(g->cap, 1);
-  if( g->q == NULL || g->orig == NULL || g->handback == NULL )
+  if( g->q == NULL || g->orig == NULL || g->handback == NULL ) {
+    ci_netif_rx_gpu_close(g);
     return -ENOMEM;
+  }
   memset(&cfg, 0, sizeof(cfg));
   cfg.device = device;
   cfg.max_socks = ni->state->n_ep_bufs;
@@ -208,8 +212,11 @@ int ci_netif_rx_gpu_open(ci_netif* ni, struct ci_netif_gpu_rx* g, int device,
     cfg.intf_hwport[i] = ni->state->intf_i_to_hwport[i];
   cfg.host_stage_bytes = (uint64_t) g->cap * 2048;
   cfg.host_stage_pkts = g->cap;
-  if( (rc = oo_gpu_rx_open(&g->gpu, &cfg)) < 0 )
+  if( (rc = oo_gpu_rx_open(&g->gpu, &cfg)) < 0 ) {
+    g->gpu = NULL;
+    ci_netif_rx_gpu_close(g);
     return rc;
+  }
   memset(&pcfg, 0, sizeof(pcfg));
   pcfg.pkt_bufs = umem;
   pcfg.pkt_bufs_bytes = umem_bytes;
@@ -218,9 +225,30 @@ int ci_netif_rx_gpu_open(ci_netif* ni, struct ci_netif_gpu_rx* g, int device,
   pcfg.sw_verify = 1;              /* AF_XDP: no NIC checksum verdict */
   pcfg.flags = OO_RX_POLL_ZERO_COPY | OO_RX_POLL_CROSSOVER;
   g->c.ni = ni;
-  if( (rc = oo_rx_poll_open(&g->poll, g->gpu, &pcfg, &ops)) < 0 )
-    oo_gpu_rx_close(g->gpu);
+  if( (rc = oo_rx_poll_open(&g->poll, g->gpu, &pcfg, &ops)) < 0 ) {
+    g->poll = NULL;
+    ci_netif_rx_gpu_close(g);
+  }
   return rc;
+}
+
+/* At stack teardown (and on ci_netif_rx_gpu_open's failure paths): the shim,
+ * the device context and the pass's queue.  Idempotent. */
+void ci_netif_rx_gpu_close(struct ci_netif_gpu_rx* g)
+{
+  if( g->poll != NULL )
+    oo_rx_poll_close(g->poll);
+  if( g->gpu != NULL )
+    oo_gpu_rx_close(g->gpu);
+  free(g->q);
+  free(g->orig);
+  free(g->handback);
+  g->poll = NULL;
+  g->gpu = NULL;
+  g->q = NULL;
+  g->orig = NULL;
+  g->handback = NULL;
+  g->cap = g->n = 0;
 }
 
 /* The shim's view of an RX / RX_DISCARD event (netif_event.c:1717-1736,

@@ -204,6 +204,7 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_group_share_ops": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_group_gather_rccl": (ctypes.c_int, [_P, _P, _U32, _P, ctypes.POINTER(_U32), _P]),
     "oo_gpu_rx_group_sum_counters": (ctypes.c_int, [_P, _P, _P]),
+    "oo_gpu_rx_group_uses_rccl": (ctypes.c_int, [_P]),
 }
 
 _lib = None

@@ -1169,7 +1169,10 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   set_groups(A, WA, CLAIM_GROUPS, 0u);
   set_tiles_dyn(A, n, WA, c->body_tail, 1);
   A.dyn = B.dyn = 1u;
-  if (oo_rx_launch_win(&B, (int)blocks_b, s) != 0) return -EIO;
+  if (oo_rx_launch_win(&B, (int)blocks_b, s) != 0) return -EIO;  // nothing ran: the set stays zero
+  // win_kernel is queued: it advances this set and zeroes the other, so the
+  // stream's next launch takes the other set whether body_kernel follows or not.
+  trk->parity ^= 1u;
   if ((gseq ? oo_rx_launch_body_gseq(&A, (int)blocks_a, s) : oo_rx_launch_body(&A, (int)blocks_a, s)) != 0)
     return -EIO;
   return 0;
@@ -1243,9 +1246,8 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
       c->len_hint ? c->len_hint <= (uint32_t)oo_rx::HB_BYTES : P.frames_bytes <= (uint64_t)oo_rx::HB_BYTES * n;
   const bool split = c->kmode == 3 || (c->kmode == 0 && window_frames && n >= (1u << 20));
   if (!tx && split && split_fits && c->grid_win > 0 && c->grid_body > 0 && c->grid_body_gseq > 0) {
-    const int rc = launch_split(c, P, n, trk, P.claim, s, short_frames);
-    if (rc != 0) return rc;  // (a launch that did not run leaves the next set zero)
-    trk->parity ^= 1u;
+    const int rc = launch_split(c, P, n, trk, P.claim, s, short_frames);  // (flips the parity)
+    if (rc != 0) return rc;
     c->last_path = (c->body_engine ? c->body_engine == 2 : short_frames) ? 4u : 3u;
     note_launch(trk);
     return 0;

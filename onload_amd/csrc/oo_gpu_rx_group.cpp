@@ -84,18 +84,29 @@ Rccl* rccl() {
 }
 
 // One table change as it travels to the other ranks (join shape): the
-// arguments of oo_gpu_rx_table_insert / _remove / oo_gpu_rx_sock_set.
-// 96 B.
+// arguments of oo_gpu_rx_table_insert / _remove / oo_gpu_rx_sock_set, and
+// the return code rank 0 got for it (a replica that gets another has
+// diverged).  96 B.
 struct GroupOp {
   uint8_t kind;  // 1 insert, 2 remove, 3 socket
   uint8_t af, proto, raddr_any;
   uint16_t lport, rport;
   int32_t sock;
-  uint32_t rsvd;
+  int32_t rc;
   uint8_t laddr[16], raddr[16];
   oo_gpu_rx_sock s;
 };
 static_assert(sizeof(GroupOp) == 96, "group op layout");
+
+// The op broadcast goes in fixed chunks through staging allocated at the
+// join: share_ops allocates nothing, so no rank can fail between two
+// collectives that the others enter.  A 16-B header (the count and rank 0's
+// flags) travels first; then ceil(count / kOpsPerChunk) body broadcasts,
+// the same number on every rank because every rank acts on the broadcast
+// count.
+constexpr uint64_t kOpsPerChunk = 8192;  // 768 KiB of ops
+constexpr uint64_t kOpsHdr = 16;
+constexpr uint32_t kOpsLost = 1;  // rank 0 could not queue an op: re-share the tables
 
 }  // namespace
 
@@ -106,9 +117,11 @@ struct oo_gpu_rx_group {
   uint32_t rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
   std::vector<GroupOp> ops;       // rank 0's changes since the last share_ops
-  void* d_ops = nullptr;          // device staging for the op broadcast
-  uint64_t d_ops_cap = 0;
+  bool ops_lost = false;          // a change rank 0 applied but could not queue
+  void* d_ops = nullptr;          // device staging for the op broadcast: header + one chunk
+  std::vector<GroupOp> h_ops;     // host staging for one chunk
   void* d_img = nullptr;          // device staging for the table image
+  uint64_t img_bytes = 0;
 };
 
 namespace {
@@ -126,16 +139,18 @@ int apply_op(oo_gpu_rx_ctx* c, const GroupOp& o) {
 // Applies one change to every local member in order (and queues it for
 // the other ranks in the join shape): the first member's return code; the
 // replicas agree, and a member that does not is reported as -EIO.
-int group_change(oo_gpu_rx_group* g, const GroupOp& o) {
+int group_change(oo_gpu_rx_group* g, GroupOp o) {
   if (g->m.empty()) return -EINVAL;
-  if (g->nranks > 1 && g->rank != 0) return -EPERM;  // rank 0 owns the tables
+  if (g->comm != nullptr && g->rank != 0) return -EPERM;  // rank 0 owns the tables
   const int rc = apply_op(g->m[0], o);
   for (size_t i = 1; i < g->m.size(); ++i)
     if (apply_op(g->m[i], o) != rc) return -EIO;
-  if (g->nranks > 1 && g->rank == 0) {
+  if (g->comm != nullptr) {
+    o.rc = rc;
     try {
       g->ops.push_back(o);
     } catch (...) {
+      g->ops_lost = true;  // the next share_ops fails on every rank
       return -ENOMEM;
     }
   }
@@ -225,9 +240,28 @@ int oo_gpu_rx_group_join(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32
   if (rc != 0) return rc;
   g->rank = rank;
   g->nranks = nranks;
+  // Every buffer a collective call needs is allocated here, before the
+  // communicator exists: the collective calls allocate nothing, so a rank
+  // never leaves one of them early on a local allocation failure.
+  g->img_bytes = oo_gpu_rx_table_image_bytes(g->m[0]);
+  try {
+    g->h_ops.resize(kOpsPerChunk);
+  } catch (...) {
+    group_free(g);
+    return -ENOMEM;
+  }
+  if (hipSetDevice(cfg->device) != hipSuccess) {
+    group_free(g);
+    return -ENODEV;
+  }
+  if (hipMalloc(&g->d_ops, kOpsHdr + sizeof(GroupOp) * kOpsPerChunk) != hipSuccess ||
+      hipMalloc(&g->d_img, g->img_bytes) != hipSuccess) {
+    group_free(g);
+    return -ENOMEM;
+  }
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
-  if (hipSetDevice(cfg->device) != hipSuccess || r->init_rank(&g->comm, (int)nranks, u, (int)rank) != ncclSuccess) {
+  if (r->init_rank(&g->comm, (int)nranks, u, (int)rank) != ncclSuccess) {
     g->comm = nullptr;
     group_free(g);
     return -EIO;
@@ -328,73 +362,88 @@ int oo_gpu_rx_group_gather(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards,
   return 0;
 }
 
+// The join shape's collectives.  Every rank enters every collective of a
+// call -- their number depends only on values all ranks share -- and a
+// local failure is reported after the last of them, never by leaving early.
+// A group opened in one process has no communicator: there they do nothing
+// (one member is its own rank 0).  A joined group of one rank runs the same
+// RCCL calls as a larger one (broadcasts and all-reduce of one rank, the
+// gather as a send/receive pair to itself).
+
 int oo_gpu_rx_group_share_tables(oo_gpu_rx_group* g, void* stream) {
   if (g == nullptr || g->m.size() != 1) return -EINVAL;
-  if (g->nranks == 1) return 0;
+  if (g->comm == nullptr) return g->nranks == 1 ? 0 : -ENOSYS;
   Rccl* r = rccl();
-  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
+  if (r == nullptr) return -ENOSYS;
   oo_gpu_rx_ctx* c = g->m[0];
-  const uint64_t bytes = oo_gpu_rx_table_image_bytes(c);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
-  if (g->d_img == nullptr && hipMalloc(&g->d_img, bytes) != hipSuccess) return -ENOMEM;
   int rc = 0;
-  if (g->rank == 0) rc = oo_gpu_rx_table_export(c, g->d_img, bytes, stream);
-  if (rc != 0) return rc;
-  if (r->bcast(g->d_img, g->d_img, bytes, ncclUint8, 0, g->comm, s) != ncclSuccess) return -EIO;
-  if (g->rank != 0) rc = oo_gpu_rx_table_import(c, g->d_img, bytes, stream);
-  g->ops.clear();  // rank 0's changes so far are in the image
+  if (g->rank == 0) rc = oo_gpu_rx_table_export(c, g->d_img, g->img_bytes, stream);
+  // (rank 0 joins the broadcast even when its export failed: the others
+  // then import an image whose header check fails, and every rank errs)
+  if (r->bcast(g->d_img, g->d_img, g->img_bytes, ncclUint8, 0, g->comm, s) != ncclSuccess)
+    rc = rc ? rc : -EIO;
+  if (g->rank != 0) rc = oo_gpu_rx_table_import(c, g->d_img, g->img_bytes, stream);
+  if (hipStreamSynchronize(s) != hipSuccess) rc = rc ? rc : -EIO;
+  if (g->rank == 0) {
+    g->ops.clear();  // rank 0's changes so far are in the image
+    g->ops_lost = false;
+  }
   return rc;
 }
 
 int oo_gpu_rx_group_share_ops(oo_gpu_rx_group* g, void* stream) {
   if (g == nullptr || g->m.size() != 1) return -EINVAL;
-  if (g->nranks == 1) return 0;
+  if (g->comm == nullptr) return g->nranks == 1 ? 0 : -ENOSYS;
   Rccl* r = rccl();
-  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
+  if (r == nullptr) return -ENOSYS;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
-  // The count, then the ops (96 B each), from rank 0.
-  uint64_t cnt = g->rank == 0 ? g->ops.size() : 0;
-  const uint64_t need = sizeof(uint64_t) + sizeof(GroupOp) * std::max<uint64_t>(cnt, 1);
-  if (g->d_ops_cap < need) {
-    if (g->d_ops) (void)hipFree(g->d_ops);
-    g->d_ops = nullptr;
-    g->d_ops_cap = 0;
-  }
-  if (g->d_ops == nullptr) {
-    const uint64_t cap = std::max<uint64_t>(need, 1u << 20);
-    if (hipMalloc(&g->d_ops, cap) != hipSuccess) return -ENOMEM;
-    g->d_ops_cap = cap;
-  }
-  if (g->rank == 0 &&
-      hipMemcpyAsync(g->d_ops, &cnt, sizeof(cnt), hipMemcpyHostToDevice, s) != hipSuccess)
-    return -EIO;
-  if (r->bcast(g->d_ops, g->d_ops, sizeof(cnt), ncclUint8, 0, g->comm, s) != ncclSuccess ||
-      hipMemcpyAsync(&cnt, g->d_ops, sizeof(cnt), hipMemcpyDeviceToHost, s) != hipSuccess ||
+  int err = 0;
+  auto fail = [&err](int e) {
+    if (err == 0) err = e;
+  };
+  // The header: the count and rank 0's flags.
+  uint64_t hdr[2] = {g->rank == 0 ? (uint64_t)g->ops.size() : 0,
+                     g->rank == 0 && g->ops_lost ? kOpsLost : 0u};
+  if (g->rank == 0 && hipMemcpyAsync(g->d_ops, hdr, kOpsHdr, hipMemcpyHostToDevice, s) != hipSuccess)
+    fail(-EIO);
+  if (r->bcast(g->d_ops, g->d_ops, kOpsHdr, ncclUint8, 0, g->comm, s) != ncclSuccess) fail(-EIO);
+  if (hipMemcpyAsync(hdr, g->d_ops, kOpsHdr, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
-    return -EIO;
-  if (cnt == 0) return 0;
-  if (sizeof(uint64_t) + sizeof(GroupOp) * cnt > g->d_ops_cap) return -ENOMEM;  // (the others' buffer)
-  uint8_t* body = static_cast<uint8_t*>(g->d_ops) + sizeof(uint64_t);
-  std::vector<GroupOp> in;
-  try {
-    in.resize(cnt);
-  } catch (...) {
-    return -ENOMEM;
+    fail(-EIO);
+  if (err != 0) return err;  // no rank has a count it can trust: none goes on
+  const uint64_t cnt = hdr[0];
+  uint8_t* body = static_cast<uint8_t*>(g->d_ops) + kOpsHdr;
+  for (uint64_t at = 0; at < cnt; at += kOpsPerChunk) {
+    const uint64_t k = std::min<uint64_t>(kOpsPerChunk, cnt - at);
+    const uint64_t bytes = sizeof(GroupOp) * k;
+    if (g->rank == 0 &&
+        hipMemcpyAsync(body, g->ops.data() + at, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+      fail(-EIO);
+    if (r->bcast(body, body, bytes, ncclUint8, 0, g->comm, s) != ncclSuccess) fail(-EIO);
+    if (hipMemcpyAsync(g->h_ops.data(), body, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      fail(-EIO);
+      continue;
+    }
+    if (g->rank == 0) {
+      // rank 0 applied these at its calls: what came back must be them
+      if (memcmp(g->h_ops.data(), g->ops.data() + at, bytes) != 0) fail(-EIO);
+    } else {
+      for (uint64_t i = 0; i < k; ++i) {
+        const GroupOp& o = g->h_ops[i];
+        if (apply_op(g->m[0], o) != o.rc) fail(-EIO);  // this replica diverged
+      }
+    }
   }
-  if (g->rank == 0 &&
-      hipMemcpyAsync(body, g->ops.data(), sizeof(GroupOp) * cnt, hipMemcpyHostToDevice, s) !=
-          hipSuccess)
-    return -EIO;
-  if (r->bcast(body, body, sizeof(GroupOp) * cnt, ncclUint8, 0, g->comm, s) != ncclSuccess ||
-      hipMemcpyAsync(in.data(), body, sizeof(GroupOp) * cnt, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return -EIO;
-  if (g->rank != 0)
-    for (const GroupOp& o : in) (void)apply_op(g->m[0], o);  // rank 0 applied them at its calls
-  g->ops.clear();
-  return (int)cnt;
+  if (g->rank == 0) {
+    g->ops.clear();
+    g->ops_lost = false;
+  }
+  if (hdr[1] & kOpsLost) fail(-EIO);  // every rank: share the tables again
+  return err ? err : (int)cnt;
 }
 
 int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_out, uint32_t n,
@@ -402,32 +451,43 @@ int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_ou
   if (g == nullptr || g->m.size() != 1 || (n > 0 && d_out == nullptr)) return -EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
-  if (g->nranks == 1) {
+  if (g->comm == nullptr) {
+    if (g->nranks != 1) return -ENOSYS;
     if (d_dst != nullptr && n > 0 && d_dst != d_out &&
         hipMemcpyAsync(d_dst, d_out, sizeof(oo_gpu_rx_result) * n, hipMemcpyDefault, s) != hipSuccess)
       return -EIO;
     return 0;
   }
   Rccl* r = rccl();
-  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
-  if (g->rank == 0 && (d_dst == nullptr || counts == nullptr)) return -EINVAL;
+  if (r == nullptr) return -ENOSYS;
+  // (rank 0 without a destination is a caller error the other ranks cannot
+  // see: their sends to it never complete)
+  if (g->rank == 0 && (d_dst == nullptr || counts == nullptr || counts[0] != n)) return -EINVAL;
   if (r->group_start() != ncclSuccess) return -EIO;
   ncclResult_t e = ncclSuccess;
   if (g->rank == 0) {
     uint64_t at = 0;
     for (uint32_t k = 0; k < g->nranks; ++k) {
       const uint64_t bytes = sizeof(oo_gpu_rx_result) * (uint64_t)counts[k];
-      if (k == 0) {
+      if (k == 0 && g->nranks > 1) {
+        // rank 0's own records: a copy on the stream
         if (bytes && d_dst != d_out &&
             hipMemcpyAsync(d_dst, d_out, bytes, hipMemcpyDefault, s) != hipSuccess)
           e = ncclSystemError;
-      } else if (bytes && e == ncclSuccess) {
-        e = r->recv(reinterpret_cast<uint8_t*>(d_dst) + at, bytes, ncclUint8, (int)k, g->comm, s);
+      } else if (bytes) {
+        // the other ranks' (and, in a group of one, rank 0's own through a
+        // send to itself)
+        const ncclResult_t er = r->recv(reinterpret_cast<uint8_t*>(d_dst) + at, bytes, ncclUint8,
+                                        (int)k, g->comm, s);
+        if (e == ncclSuccess) e = er;
       }
       at += bytes;
     }
-  } else if (n > 0) {
-    e = r->send(d_out, sizeof(oo_gpu_rx_result) * (uint64_t)n, ncclUint8, 0, g->comm, s);
+  }
+  if ((g->rank != 0 || g->nranks == 1) && n > 0) {
+    const ncclResult_t er =
+        r->send(d_out, sizeof(oo_gpu_rx_result) * (uint64_t)n, ncclUint8, 0, g->comm, s);
+    if (e == ncclSuccess) e = er;
   }
   const ncclResult_t e2 = r->group_end();
   return (e == ncclSuccess && e2 == ncclSuccess) ? 0 : -EIO;
@@ -435,14 +495,16 @@ int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_ou
 
 int oo_gpu_rx_group_sum_counters(oo_gpu_rx_group* g, oo_gpu_rx_counters* d_counters, void* stream) {
   if (g == nullptr || g->m.size() != 1 || d_counters == nullptr) return -EINVAL;
-  if (g->nranks == 1) return 0;
+  if (g->comm == nullptr) return g->nranks == 1 ? 0 : -ENOSYS;
   Rccl* r = rccl();
-  if (r == nullptr || g->comm == nullptr) return -ENOSYS;
+  if (r == nullptr) return -ENOSYS;
   if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
   return r->allreduce(d_counters, d_counters, OO_RX_R_COUNT, ncclUint32, ncclSum, g->comm,
                       static_cast<hipStream_t>(stream)) == ncclSuccess
              ? 0
              : -EIO;
 }
+
+int oo_gpu_rx_group_uses_rccl(const oo_gpu_rx_group* g) { return g && g->comm ? 1 : 0; }
 
 }  // extern "C"

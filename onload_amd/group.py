@@ -93,6 +93,11 @@ class GpuRxGroup:
     def rank(self) -> int:
         return int(self._lib.oo_gpu_rx_group_rank(self._g))
 
+    @property
+    def uses_rccl(self) -> bool:
+        """True for a joined group: its collectives run over librccl."""
+        return bool(self._lib.oo_gpu_rx_group_uses_rccl(self._g))
+
     def close(self) -> None:
         if self._g:
             for m in self.members:

@@ -489,10 +489,26 @@ static int chunk_complete(oo_rx_poll* p, struct chunk* c, oo_rx_poll_stats* st)
        * new tables.  Its events were classified (and counted) already: only
        * the batch or the hand-back is added to the counters. */
       const oo_rx_poll_stats saved = c->st;
+      const oo_rx_poll_ev* rest = c->evs + i + 1;
+      const uint32_t nrest = c->n - i - 1;
+      oo_rx_poll_stats cls;
       uint64_t handed;
-      int rc = chunk_submit(p, c, c->evs + i + 1, c->n - i - 1, &saved);
+      uint32_t j;
+      int rc;
+      /* what the first classification of the rest counted (in saved) */
+      memset(&cls, 0, sizeof(cls));
+      for( j = 0; j < nrest; ++j )
+        (void)classify(p, &rest[j], &cls);
+      rc = chunk_submit(p, c, rest, nrest, &saved);
       handed = c->st.n_handback - saved.n_handback;
       c->st = saved;
+      if( handed ) {
+        /* the rest goes to other_ev: the caller's loop counts it itself */
+        uint64_t* a = (uint64_t*)&c->st;
+        const uint64_t* b = (const uint64_t*)&cls;
+        for( j = 0; j < sizeof(oo_rx_poll_stats) / sizeof(uint64_t); ++j )
+          a[j] -= b[j];
+      }
       c->st.n_handback += handed;
       ++c->st.n_resubmit;
       if( rc < 0 )

@@ -266,3 +266,54 @@ def test_poll_crossover(cuda, zero_copy):
         assert rec.calls[len(rec.calls) - len(tail):] == tail
         assert st["n_handback"] == n - cut
     assert st["n_batches"] >= (cut // 64) - 1
+
+
+def test_poll_table_change_then_rest_handed_back(cuda):
+    """A callback changes the tables mid-chunk with OO_RX_POLL_CROSSOVER set,
+    and the model prices the re-transformed rest of the chunk below the
+    device batch: the rest goes to other_ev, and none of it is counted by
+    the shim -- rx_evs and the discard class counters hold only
+    the events the shim itself handled."""
+    import cases
+    socks, filters = cases.order_world()
+    g = GpuRxStack(device=0, host_stage_bytes=16 << 20, host_stage_pkts=4096)
+    install(g, (socks, filters))
+    f = cases.order_frame()
+    epp = 64
+    n = 3 * epp
+    pool = np.zeros(n * 2048, np.uint8)
+    evs = np.zeros(n, poll.EV_DTYPE)
+    for i in range(n):
+        pool[i * 2048 + 192:i * 2048 + 192 + len(f)] = np.frombuffer(f, np.uint8)
+        # every 5th event a bad-FCS discard: released, counted in its class
+        evs[i] = (i, 192, len(f), poll.EV_SOP, poll.DISCARD_ETH_FCS_ERR if i % 5 == 4 else 0, 0, 0)
+    cut = 30  # the rest of chunk 0 (33 events) is re-priced and loses
+    removed = []
+
+    class Closer(Recorder):
+        def post_future(self, i, r, fu):
+            if i == cut and not removed:
+                removed.append(g.filter_remove(*filters[0]))
+            return super().post_future(i, r, fu)
+
+        def full_handler(self, i, r):
+            if i == cut and not removed:
+                removed.append(g.filter_remove(*filters[0]))
+            super().full_handler(i, r)
+
+    # per chunk: fixed = 40 frames' worth of the CPU's per-frame saving
+    per = {"cpu_pkt_ps": 20000, "cpu_byte_ps": 0, "gpu_pkt_ps": 10000, "gpu_byte_ps": 0,
+           "gpu_fixed_ns": 400}
+    rec = Closer()
+    p = poll.RxPoll(g, pool, 2048, epp, True, rec, crossover=per)
+    assert p.poll(evs) == n
+    assert removed == [0]
+    st = p.stats.as_dict()
+    rest = set(range(cut + 1, epp))
+    assert [c for c in rec.calls if c[0] == "other"] == [("other", i) for i in sorted(rest)]
+    assert st["n_handback"] == len(rest) and st["n_other"] == len(rest)
+    fcs = [i for i in range(n) if i % 5 == 4]
+    assert st["rx_discard_crc_bad"] == len([i for i in fcs if i not in rest])
+    assert st["rx_evs"] == len([i for i in range(n) if i % 5 != 4 and i not in rest])
+    p.close()
+    g.close()

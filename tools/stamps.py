@@ -109,10 +109,18 @@ def main() -> None:
     dm = ph[:, 8] != 0
     if dm.any():
         q = ph[dm]
-        res["demux_us_mean"] = {"occ_words": float(((q[:, 8] - q[:, 2]) * ns).mean() / 1e3),
-                                "to_walks": float(((q[:, 9] - q[:, 8]) * ns).mean() / 1e3),
-                                "walks": float(((q[:, 10] - q[:, 9]) * ns).mean() / 1e3),
-                                "after_walks": float(((q[:, 3] - q[:, 10]) * ns).mean() / 1e3)}
+
+        def phase(i, j):
+            # a phase whose start or end stamp is missing (0: the build or
+            # the tile did not reach it) is reported as missing, never as a
+            # difference against zero
+            ok = (q[:, i] != 0) & (q[:, j] != 0)
+            if not ok.any():
+                return {"us": None, "tiles": 0, "missing": int(len(q))}
+            return {"us": float(((q[ok, j] - q[ok, i]) * ns).mean() / 1e3), "tiles": int(ok.sum()),
+                    "missing": int((~ok).sum())}
+        res["demux_us_mean"] = {"occ_words": phase(2, 8), "to_walks": phase(8, 9),
+                                "walks": phase(9, 10), "after_walks": phase(10, 3)}
         # The state-machine walk stamps its step count in slot 11 (+1e6).
         fsm = dm & (ph[:, 11] >= 1000000) & (ph[:, 11] < 2000000)
         if fsm.any():
