@@ -74,6 +74,8 @@ def parse_args(argv=None):
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
     ap.add_argument("--n", type=int, default=0, help="packets per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--align", type=int, default=64,
+                    help="frame alignment in the packed buffer (diagnostics: 64 is the workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--steady", type=int, default=200,
                     help="side measurement after the timed region: this many more launches, "
@@ -207,7 +209,7 @@ def run_rank(args) -> None:
     first, n = shards.shard_for(cfg, seed, n_total, rank, world)
     t0 = time.time()
     filters, socks = pktgen.world(cfg)
-    buf, desc = pktgen.generate(cfg, n, seed=seed, first=first)
+    buf, desc = pktgen.generate(cfg, n, seed=seed, first=first, align=args.align)
     log(f"[rank {rank}] packets [{first}, {first + n}) ({buf.nbytes / 1e9:.2f} GB) "
         f"generated in {time.time() - t0:.1f}s")
 

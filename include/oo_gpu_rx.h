@@ -238,6 +238,19 @@ uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* ctx);
  * per-group-sequence body_kernel; 0 none yet.  For measurements: which
  * kernels a timed launch's duration covers. */
 uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* ctx);
+/* Table maintenance so far: flushes of queued changes to the device, and how
+ * the key index followed each -- rebuilt from the tables, or updated for the
+ * flushed ops' keys alone (a flush of at most 1024 filter ops with no
+ * socket change) -- and whether it answers lookups now (waits for the
+ * device).  For tests and measurements. */
+typedef struct oo_gpu_rx_table_stats {
+  uint64_t flushes;
+  uint64_t index_rebuilds;
+  uint64_t index_updates;
+  uint32_t index_on;
+  uint32_t rsvd;
+} oo_gpu_rx_table_stats;
+int oo_gpu_rx_get_table_stats(oo_gpu_rx_ctx* ctx, oo_gpu_rx_table_stats* out);
 /* Streams.  The context remembers the streams it launched on (nothing is
  * recorded per batch): a table change enqueues an event on each of them at
  * that moment and waits for it, so every stream used with the context must

@@ -109,6 +109,13 @@ class PgFilter(ctypes.Structure):
 
 
 # struct iovec (<sys/uio.h>), for the host-pure verifiers.
+class TableStats(ctypes.Structure):
+    """oo_gpu_rx_table_stats."""
+    _fields_ = [("flushes", ctypes.c_uint64), ("index_rebuilds", ctypes.c_uint64),
+                ("index_updates", ctypes.c_uint64), ("index_on", ctypes.c_uint32),
+                ("rsvd", ctypes.c_uint32)]
+
+
 class IoVec(ctypes.Structure):
     _fields_ = [("iov_base", ctypes.c_void_p), ("iov_len", ctypes.c_size_t)]
 
@@ -157,6 +164,7 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_stream_done": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_table_gen": (ctypes.c_uint64, [_P]),
     "oo_gpu_rx_last_path": (ctypes.c_uint32, [_P]),
+    "oo_gpu_rx_get_table_stats": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_set_len_hint": (ctypes.c_int, [_P, _U32]),
     "oo_gpu_rx_set_tuning": (ctypes.c_int, [_P, ctypes.POINTER(Tuning)]),
     "oo_gpu_rx_process_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _P]),

@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <new>
 #include <unordered_map>
+#include <unordered_set>
+#include <string>
 #include <vector>
 
 #include "oo_rx_device.h"
@@ -46,7 +48,8 @@ extern "C" int oo_rx_body_blocks_per_cu_gseq(void);
 extern "C" int oo_rx_launch_body_gseq(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
                                    const uint32_t* d_lev_end, uint32_t nlev, uint32_t gen,
-                                   hipStream_t s);
+                                   uint32_t kx_mode, uint32_t* kx_req, hipStream_t s);
+extern "C" uint32_t oo_table_threads(void);
 extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s);
 extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s);
 extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s);
@@ -146,6 +149,7 @@ struct Tracked {
 // the kernel that read it has finished (ev).
 struct OpStage {
   TableOp* h = nullptr;
+  TableOp* hd = nullptr;  // h as the device addresses it (small flushes read it in place)
   TableOp* d = nullptr;
   hipEvent_t ev = nullptr;
   bool pending = false;
@@ -210,6 +214,16 @@ struct oo_gpu_rx_ctx {
   hipStream_t tables_stream = nullptr;
   OpStage stage[2];
   int stage_next = 0;
+  // Key-index maintenance (oo_table_kernel.hip): a flush of at most
+  // oo_table_threads() filter ops updates the ops' own keys in the ops
+  // kernel; anything else rebuilds the index.  kx_full: the pending ops need
+  // the rebuild (a socket change, or an op whose tuple is not its socket's);
+  // h_kx_req: host memory a kernel sets when the index needs one (it is off,
+  // or overflowed).
+  bool kx_full = false;
+  uint32_t* h_kx_req = nullptr;
+  uint32_t* d_kx_req = nullptr;
+  uint64_t n_flush = 0, n_kx_full = 0, n_kx_inc = 0;
   Tracked track[NTRACK];
   uint64_t lru = 0;
   uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros, the sink, the hwport table
@@ -259,6 +273,14 @@ void push_op(oo_gpu_rx_ctx* c, const TableOp& op) {
     if (it != c->sock_op_at.end()) c->ops[it->second].kind = 0;  // superseded: skipped
     c->sock_op_at[op.sock] = c->ops.size();
   } else {
+    // The index keys an op's entry by its socket's fields (the slot record's);
+    // an op whose tuple differs cannot be updated incrementally.
+    const oo_gpu_rx_sock& k = c->socks[op.sock];
+    const bool same = op.af == 4 ? op.u.t.ra[0] == k.raddr_be32 && op.rport == k.rport_be16 &&
+                                       op.proto == k.protocol
+                                 : memcmp(op.u.t.ra, k.raddr6, 16) == 0 && op.rport == k.rport_be16 &&
+                                       op.lport == k.lport_be16 && op.proto == k.protocol;
+    if (!same) c->kx_full = true;
     const uint64_t af = (uint64_t)op.af << 32;
     for (uint32_t slot : c->touched) {
       auto it = c->slot_level.find(af | slot);
@@ -271,6 +293,7 @@ void push_op(oo_gpu_rx_ctx* c, const TableOp& op) {
 }
 
 void clear_ops(oo_gpu_rx_ctx* c) {
+  c->kx_full = false;
   c->ops.clear();
   c->op_level.clear();
   c->slot_level.clear();
@@ -572,6 +595,7 @@ void free_dev(oo_gpu_rx_ctx* c) {
   for (const HostReg& r : c->regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.lo));
   if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
   if (c->h_image_hdr) (void)hipHostFree(c->h_image_hdr);
+  if (c->h_kx_req) (void)hipHostFree(c->h_kx_req);
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -633,6 +657,29 @@ int order_after_batches(oo_gpu_rx_ctx* c, hipStream_t s) {
   return 0;
 }
 
+// One op per distinct index key of an incremental flush recomputes it
+// (TableOp::rsvd0 KX_OWN_*): the exact tuple, and for IPv6 the wildcard key
+// (laddr, lport, protocol) of the ra_null stages.
+void mark_kx_owners(TableOp* h, uint32_t n) {
+  std::unordered_set<std::string> seen;
+  for (uint32_t k = 0; k < n; ++k) {
+    TableOp& op = h[k];
+    if (op.kind != oo_rx::OP_INSERT && op.kind != oo_rx::OP_REMOVE) continue;
+    std::string key(reinterpret_cast<const char*>(&op.u.t), sizeof(op.u.t));
+    key.push_back((char)op.af);
+    key.push_back((char)op.proto);
+    key.append(reinterpret_cast<const char*>(&op.lport), 2);
+    std::string wild = key;
+    key.append(reinterpret_cast<const char*>(&op.rport), 2);
+    if (seen.insert(key).second) op.rsvd0 |= oo_rx::KX_OWN_EXACT;
+    if (op.af == 6) {
+      memset(&wild[16], 0, 16);  // (raddr)
+      wild.push_back('w');
+      if (seen.insert(wild).second) op.rsvd0 |= oo_rx::KX_OWN_WILD;
+    }
+  }
+}
+
 // Pending table ops -> device, on stream s: first order s after the
 // batches on other streams, then copy the ops through a pinned staging
 // buffer and apply them (table_ops), then refresh the socket fields of the
@@ -651,6 +698,13 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
   for (uint32_t i = 0; i < total; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(),
                    [c](uint32_t a, uint32_t b) { return c->op_level[a] < c->op_level[b]; });
+  // A small flush: the kernel reads the ops from the pinned staging buffer
+  // itself (no copy on the stream) and, with filter ops only and the index
+  // not asking for a rebuild, updates the index for the ops' keys.
+  const bool small = total <= oo_table_threads();
+  const bool req = c->h_kx_req != nullptr && *reinterpret_cast<volatile uint32_t*>(c->h_kx_req) != 0;
+  const bool inc = small && !c->kx_full && !c->ops_sock && !req && c->d_kx_req != nullptr &&
+                   c->T.kx4 != nullptr;
   for (uint32_t at = 0; at < total; at += OPS_CHUNK) {
     const uint32_t n = std::min(OPS_CHUNK, total - at);
     OpStage& st = c->stage[c->stage_next];
@@ -665,25 +719,37 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
     for (uint32_t k = 0; k < n; ++k) {
       const uint32_t i = order[at + k];
       h[k] = c->ops[i];
+      h[k].rsvd0 = 0;
       if (k > 0 && c->op_level[i] != c->op_level[order[at + k - 1]]) lev_end[nlev++] = k;
     }
     lev_end[nlev++] = n;
-    if (hipMemcpyAsync(st.d, st.h, sizeof(TableOp) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(st.d + OPS_CHUNK, lev_end, sizeof(uint32_t) * nlev, hipMemcpyHostToDevice,
-                       s) != hipSuccess ||
-        oo_table_launch_ops(&c->T, st.d, reinterpret_cast<const uint32_t*>(st.d + OPS_CHUNK), nlev,
-                            c->gen, s) != 0 ||
+    if (inc) mark_kx_owners(h, n);
+    const TableOp* d_ops = st.d;
+    const uint32_t* d_lev = reinterpret_cast<const uint32_t*>(st.d + OPS_CHUNK);
+    bool ok = true;
+    if (small && st.hd != nullptr) {
+      d_ops = st.hd;
+      d_lev = reinterpret_cast<const uint32_t*>(st.hd + OPS_CHUNK);
+    } else {
+      ok = hipMemcpyAsync(st.d, st.h, sizeof(TableOp) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
+           hipMemcpyAsync(st.d + OPS_CHUNK, lev_end, sizeof(uint32_t) * nlev, hipMemcpyHostToDevice,
+                          s) == hipSuccess;
+    }
+    if (!ok || oo_table_launch_ops(&c->T, d_ops, d_lev, nlev, c->gen, inc ? 1u : 0u, c->d_kx_req, s) != 0 ||
         hipEventRecord(st.ev, s) != hipSuccess) {
       c->failed = true;  // this chunk or an earlier one may have reached the device
       return -EIO;
     }
     st.pending = true;
   }
+  if (!inc && c->h_kx_req != nullptr) *reinterpret_cast<volatile uint32_t*>(c->h_kx_req) = 0;
   if ((c->ops_sock && oo_table_launch_refresh(&c->T, c->gen, s) != 0) ||
-      oo_table_launch_kx(&c->T, s) != 0) {
+      (!inc && oo_table_launch_kx(&c->T, s) != 0)) {
     c->failed = true;
     return -EIO;
   }
+  ++c->n_flush;
+  ++(inc ? c->n_kx_inc : c->n_kx_full);
   clear_ops(c);
   ++c->gen;
   ++c->tables_gen;
@@ -867,8 +933,12 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   for (OpStage& st : c->stage)
     ok = ok && hipHostMalloc(&st.h, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK,
                              hipHostMallocDefault) == hipSuccess &&
+         hipHostGetDevicePointer(reinterpret_cast<void**>(&st.hd), st.h, 0) == hipSuccess &&
          hipMalloc(&st.d, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK) == hipSuccess &&
          hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipHostMalloc(&c->h_kx_req, 128, hipHostMallocDefault) == hipSuccess &&
+       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_kx_req), c->h_kx_req, 0) == hipSuccess;
+  if (ok) *c->h_kx_req = 0;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {
     c->stage_bytes = cfg->host_stage_bytes;
     c->stage_pkts = cfg->host_stage_pkts;
@@ -975,6 +1045,21 @@ int oo_gpu_rx_sock_set(oo_gpu_rx_ctx* c, int32_t id, const oo_gpu_rx_sock* s) {
 uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* c) { return c == nullptr ? 0 : c->changes; }
 
 uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* c) { return c == nullptr ? 0 : c->last_path; }
+
+int oo_gpu_rx_get_table_stats(oo_gpu_rx_ctx* c, oo_gpu_rx_table_stats* out) {
+  if (c == nullptr || out == nullptr) return -EINVAL;
+  memset(out, 0, sizeof(*out));
+  out->flushes = c->n_flush;
+  out->index_rebuilds = c->n_kx_full;
+  out->index_updates = c->n_kx_inc;
+  if (!has_dev(c)) return 0;
+  uint32_t ok = 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&ok, c->T.kx_ok, sizeof(ok), hipMemcpyDeviceToHost) != hipSuccess)
+    return -EIO;
+  out->index_on = ok;
+  return 0;
+}
 
 int oo_gpu_rx_sync_tables(oo_gpu_rx_ctx* c, void* stream) {
   if (c == nullptr) return -EINVAL;

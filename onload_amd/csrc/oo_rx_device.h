@@ -139,6 +139,15 @@ static_assert(sizeof(TableOp) == 64, "table op layout");
 // always empty (a two-bucket load at the end reads it).  Value 0: empty.
 constexpr uint32_t KX_VALID = 0x80000000u;
 constexpr uint32_t KX_FB = 0x40000000u;
+// A key that lost its last match since the index was built keeps its entry
+// with this value (incremental maintenance, oo_table_kernel.hip): a lookup
+// that meets it walks the table, and an entry never turns empty between two
+// rebuilds, so no key's run gains an empty entry before the key.
+constexpr uint32_t KX_DEAD = KX_FB;
+// TableOp::rsvd0 bits set by the host for an incremental flush: the op owns
+// the recomputation of its exact key / (IPv6) its wildcard key (one op per
+// distinct key of the flush).
+constexpr uint8_t KX_OWN_EXACT = 1, KX_OWN_WILD = 2;
 constexpr uint32_t KX_OVF = 64;
 constexpr uint32_t KX_PAD4 = KX_OVF + 2, KX_PAD6 = KX_OVF + 1;
 constexpr uint32_t KX_WALK_MAX = 4096;  // a longer build walk turns the index off

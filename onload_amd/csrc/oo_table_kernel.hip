@@ -222,20 +222,6 @@ __device__ __forceinline__ void apply_op(const DevTables& T, const TableOp& op, 
   }  // kind 0: a socket op superseded by a later one
 }
 
-// The ops of one flush chunk: level L is ops[lev_end[L-1], lev_end[L]).
-constexpr int TABLE_THREADS = 1024;
-__global__ __launch_bounds__(TABLE_THREADS) void table_ops(DevTables T, const TableOp* ops,
-                                                           const uint32_t* lev_end, uint32_t nlev,
-                                                           uint32_t gen) {
-  uint32_t start = 0;
-  for (uint32_t L = 0; L < nlev; ++L) {
-    const uint32_t end = lev_end[L];
-    for (uint32_t k = start + threadIdx.x; k < end; k += TABLE_THREADS) apply_op(T, ops[k], gen);
-    __syncthreads();  // the next level sees this one's slots
-    start = end;
-  }
-}
-
 // Slots whose socket changed in flush `gen` take its new fields (IPv4: every
 // slot that is not EMPTY keeps its id; IPv6: occupied slots).
 __global__ __launch_bounds__(256) void table_refresh(DevTables T, uint32_t gen) {
@@ -479,6 +465,152 @@ __global__ __launch_bounds__(256) void table_kx(DevTables T) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Incremental key-index maintenance (a flush of filter ops only, one chunk,
+// the index on).  After the flush's ops, the answers of the ops' own keys are
+// walked again and written into the index; no other key's answer can have
+// changed:
+//  * a slot an insert fills was EMPTY or a tombstone.  A walk of another key
+//    passes a filled tombstone as it passed the tombstone, and the new entry
+//    is not that key's match (keys are exact tuples; the first probe's
+//    unchecked lport is the Local Port Recovery Property's,
+//    netif_table.c:276-290).  A walk that ended at the filled EMPTY slot had
+//    no match past it: every entry past a slot on its key's probe sequence
+//    raised that slot's route count when it went in (:349-376), so the slot
+//    could not be EMPTY while such an entry was there.
+//  * a remove turns the entry's slot, and passed tombstones whose route
+//    count drops to 0, into tombstones or EMPTY slots; by the same count
+//    argument no other key has a match past a slot that becomes EMPTY.
+// Socket-field changes, ops whose tuple is not their socket's (the host
+// checks both) and larger flushes take the full rebuild instead.
+// A key that lost its last match keeps its entry as KX_DEAD (its lookups walk
+// the table); an overflow, a long walk or an index that is already off asks
+// the host for a full rebuild at the next flush (kx_req, host memory).
+
+// The value word of the key's entry, or nullptr when the key has none (the
+// first empty entry along its run ends the search, as it ends a lookup).
+__device__ uint32_t* kx_find4(const DevTables& T, uint32_t proto, uint32_t la, uint32_t ra,
+                              uint32_t ports) {
+  uint32_t* base = T.kx4 + (proto == 6u ? (size_t)(T.kx_nb4 + KX_PAD4) * 8u : 0u);
+  const uint32_t b = kx_hash(la, 0, 0, 0, ra, 0, 0, 0, ports, 0) & (T.kx_nb4 - 1u);
+  for (uint32_t q = b; q < T.kx_nb4 + KX_OVF; ++q) {
+    for (uint32_t e = 0; e < 2; ++e) {
+      uint32_t* ent = base + (size_t)q * 8u + e * 4u;
+      if (ent[3] == 0u) return nullptr;
+      if (ent[0] == la && ent[1] == ra && ent[2] == ports) return ent + 3;
+    }
+  }
+  return nullptr;
+}
+
+__device__ uint32_t* kx_find6(const DevTables& T, const uint32_t la[4], const uint32_t ra[4],
+                              uint32_t ports, uint32_t pw) {
+  const uint32_t b = kx_hash(la[0], la[1], la[2], la[3], ra[0], ra[1], ra[2], ra[3], ports, pw) &
+                     (T.kx_ne6 - 1u);
+  for (uint32_t q = b; q < T.kx_ne6 + KX_OVF; ++q) {
+    uint32_t* ent = T.kx6 + (size_t)q * 16u;
+    if (ent[10] == 0u) return nullptr;
+    if (ent[0] == la[0] && ent[1] == la[1] && ent[2] == la[2] && ent[3] == la[3] &&
+        ent[4] == ra[0] && ent[5] == ra[1] && ent[6] == ra[2] && ent[7] == ra[3] &&
+        ent[8] == ports && ent[9] == pw)
+      return ent + 10;
+  }
+  return nullptr;
+}
+
+// One index key an op owns, between the two phases.
+struct KxKey {
+  uint32_t la[4], ra[4], ports, pw, val;
+  bool claim;  // phase 2: the key has no entry yet and a live answer
+};
+
+__device__ __forceinline__ void kx_request_full(uint32_t* kx_req) {
+  __hip_atomic_store(kx_req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Phase 1 for one key: its walk's answer, written in place when the key has
+// an entry.
+__device__ void kx_key_phase1(const DevTables& T, uint32_t af, uint32_t proto, bool wild,
+                              KxKey& k, uint32_t* kx_req) {
+  KxWalk w;
+  uint32_t id = 0;
+  uint32_t* at;
+  if (af == 4) {
+    w = kx_walk4(T, k.la[0], k.ports & 0xffffu, k.ra[0], k.ports >> 16, proto);
+    if (w.n) id = T.slot4[w.first].id_state & ID_MASK;
+  } else {
+    w = kx_walk6(T, k.la, k.ports & 0xffffu, k.ra, k.ports >> 16, proto, wild);
+    if (w.n) id = (uint32_t)T.slot6[w.first].id;
+  }
+  if (!w.ok) {
+    kx_off(T);
+    kx_request_full(kx_req);
+    return;
+  }
+  k.val = w.n ? kx_value(w, id, proto) : KX_DEAD;
+  at = af == 4 ? kx_find4(T, proto, k.la[0], k.ra[0], k.ports) : kx_find6(T, k.la, k.ra, k.ports, k.pw);
+  if (at != nullptr) *at = k.val;  // (a dead key stays in place: lookups walk)
+  else k.claim = w.n != 0;
+}
+
+// The ops of one flush chunk: level L is ops[lev_end[L-1], lev_end[L]).
+// kx_mode 1: then the incremental index update for the ops (at most one per
+// thread) that own a key.
+constexpr int TABLE_THREADS = 1024;
+__global__ __launch_bounds__(TABLE_THREADS) void table_ops(DevTables T, const TableOp* ops,
+                                                           const uint32_t* lev_end, uint32_t nlev,
+                                                           uint32_t gen, uint32_t kx_mode,
+                                                           uint32_t* kx_req) {
+  __shared__ uint32_t kx_on;
+  if (kx_mode && threadIdx.x == 0) kx_on = T.kx_ok[0];
+  uint32_t start = 0;
+  for (uint32_t L = 0; L < nlev; ++L) {
+    const uint32_t end = lev_end[L];
+    for (uint32_t k = start + threadIdx.x; k < end; k += TABLE_THREADS) apply_op(T, ops[k], gen);
+    __syncthreads();  // the next level sees this one's slots (and kx_on is set)
+    start = end;
+  }
+  if (!kx_mode) return;
+  __syncthreads();  // (kx_on, also for a chunk of no levels)
+  if (kx_on == 0u) {  // off since the last rebuild: only a rebuild brings it back
+    if (threadIdx.x == 0) kx_request_full(kx_req);
+    return;
+  }
+  // Phase 1: every owned key's answer; keys with an entry are updated.
+  KxKey key[2];
+  uint32_t af = 0, proto = 0;
+  key[0].claim = key[1].claim = false;
+  if (threadIdx.x < start) {  // (start: the chunk's op count, at most TABLE_THREADS)
+    const TableOp op = ops[threadIdx.x];
+    af = op.af;
+    proto = op.proto;
+    if ((op.kind == OP_INSERT || op.kind == OP_REMOVE) && (proto == 6u || proto == 17u)) {
+      for (int i = 0; i < 4; ++i) {
+        key[0].la[i] = key[1].la[i] = af == 4 && i ? 0u : op.u.t.la[i];
+        key[0].ra[i] = af == 4 && i ? 0u : op.u.t.ra[i];
+        key[1].ra[i] = 0u;
+      }
+      key[0].ports = (uint32_t)op.lport | ((uint32_t)op.rport << 16);
+      key[0].pw = af == 6 ? proto : 0u;
+      key[1].ports = op.lport;
+      key[1].pw = proto | 0x100u;
+      if (op.rsvd0 & KX_OWN_EXACT) kx_key_phase1(T, af, proto, false, key[0], kx_req);
+      if (af == 6 && (op.rsvd0 & KX_OWN_WILD)) kx_key_phase1(T, af, proto, true, key[1], kx_req);
+    }
+  }
+  __syncthreads();  // every search is done before any claim writes a key
+  // Phase 2: new keys claim the first free entry of their run.
+  for (int j = 0; j < 2; ++j) {
+    if (!key[j].claim) continue;
+    const bool ok = af == 4 ? kx_put4(T, proto, key[j].la[0], key[j].ra[0], key[j].ports, key[j].val)
+                            : kx_put6(T, key[j].la, key[j].ra, key[j].ports, key[j].pw, key[j].val);
+    if (!ok) {
+      kx_off(T);
+      kx_request_full(kx_req);
+    }
+  }
+}
+
 }  // namespace oo_rx
 
 namespace {
@@ -488,13 +620,17 @@ int grid_for(uint32_t items) {
 }
 }  // namespace
 
+// kx_mode 1 (at most TABLE_THREADS ops): the incremental index update after
+// the ops; kx_req is host memory the kernel sets to ask for a full rebuild.
 extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::TableOp* d_ops,
                                    const uint32_t* d_lev_end, uint32_t nlev, uint32_t gen,
-                                   hipStream_t s) {
+                                   uint32_t kx_mode, uint32_t* kx_req, hipStream_t s) {
   hipLaunchKernelGGL(oo_rx::table_ops, dim3(1), dim3(oo_rx::TABLE_THREADS), 0, s, *T, d_ops,
-                     d_lev_end, nlev, gen);
+                     d_lev_end, nlev, gen, kx_mode, kx_req);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+extern "C" uint32_t oo_table_threads(void) { return oo_rx::TABLE_THREADS; }
 
 extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s) {
   hipLaunchKernelGGL(oo_rx::table_refresh, dim3(grid_for(T->ip4_mask + T->ip6_mask + 2u)),

@@ -194,6 +194,15 @@ class GpuRxStack:
         """oo_gpu_rx_table_gen: table and socket changes made so far."""
         return int(self._lib.oo_gpu_rx_table_gen(self._ctx))
 
+    def table_stats(self) -> dict:
+        """oo_gpu_rx_get_table_stats: flushes, index rebuilds / incremental
+        updates, and whether the key index is on (waits for the device)."""
+        st = _abi.TableStats()
+        rc = self._lib.oo_gpu_rx_get_table_stats(self._ctx, ctypes.byref(st))
+        if rc:
+            raise OSError(-rc, "oo_gpu_rx_get_table_stats")
+        return {n: int(getattr(st, n)) for n, _ in st._fields_ if n != "rsvd"}
+
     def last_path(self) -> int:
         """oo_gpu_rx_last_path: the last batch's kernels (1 / 2 rx_kernel
         instances, 3 / 4 the split transform with the lockstep / sequences

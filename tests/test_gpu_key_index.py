@@ -217,3 +217,96 @@ def test_walks_alone(cuda, kernel, monkeypatch):
         buf, desc = pktgen.generate(config, n, first=4242 * config, nthreads=NTHREADS)
         _check(g, o, buf, desc)
         g.close()
+
+
+def _churn_ops(stacks, filters, idx, remove):
+    for i in idx:
+        f = filters[i]
+        n = 4 if f.af == 4 else 16
+        ra = None if f.raddr_any else bytes(f.raddr)[:n]
+        for s in stacks:
+            fn = s.filter_remove_raw if remove else s.filter_insert_raw
+            rc = fn(f.sock, f.af, bytes(f.laddr)[:n], f.lport_be, ra, f.rport_be, f.proto)
+            assert rc == 0 or remove, rc
+
+
+@pytest.mark.parametrize("kernel", ["0", "3"])
+def test_incremental_index_under_churn(cuda, kernel, monkeypatch):
+    """Small flushes of filter removes and re-inserts (no socket change)
+    update the index for the flushed keys only (oo_gpu_rx_get_table_stats:
+    index_updates, no rebuild): keys that lost their last match stay as dead
+    entries that walk, re-inserted keys take their new first slot, and the
+    records equal the oracle's walks after every flush -- IPv4 and IPv6, TCP
+    and UDP (config 5's world), and keys in one full IPv4 bucket."""
+    if kernel != "0":
+        monkeypatch.setenv("OO_RX_KERNEL", kernel)
+    filters, socks = pktgen.world(5)
+    g, o = _pair()
+    g.load_world(filters, socks)
+    o.load_world(filters, socks)
+    keys4 = colliding_v4(40)
+    _install_keys((g, o), keys4, [], first_id=6000)
+    buf, desc = pktgen.generate(5, 1 << 15, first=777, nthreads=NTHREADS)
+    kbuf, kdesc = pack(_world_frames(keys4, []))
+    _check(g, o, buf, desc)
+    st0 = g.table_stats()
+    assert st0["index_on"] == 1
+    rng = np.random.default_rng(9)
+    removed = set()
+    for r in range(6):
+        out = rng.choice(len(filters), 60, replace=False)
+        out = [i for i in out if i not in removed]
+        _churn_ops((g, o), filters, out, remove=True)
+        removed.update(out)
+        back = rng.choice(sorted(removed), min(len(removed), 40), replace=False)
+        _churn_ops((g, o), filters, back, remove=False)
+        removed.difference_update(back)
+        # keys of the full bucket: some go, some come back
+        for j, (la, lp) in enumerate(keys4):
+            if (j + r) % 3 == 0:
+                for s in (g, o):
+                    s.filter_remove(6000 + j, 4, la, lp, None, 0, 17)
+            elif (j + r) % 3 == 1:
+                for s in (g, o):
+                    s.filter_remove(6000 + j, 4, la, lp, None, 0, 17)
+                    assert s.filter_insert(6000 + j, 4, la, lp, None, 0, 17) == 0
+        _check(g, o, buf, desc)
+        _check(g, o, kbuf, kdesc)
+    st = g.table_stats()
+    assert st["index_updates"] - st0["index_updates"] >= 10, st  # (two flushes a round)
+    assert st["index_rebuilds"] == st0["index_rebuilds"], st
+    assert st["index_on"] == 1
+    g.close()
+
+
+def test_incremental_index_falls_back_to_rebuild(cuda):
+    """A socket change in a flush, or an op whose tuple is not its socket's,
+    rebuilds the index; an index turned off by an overflow is rebuilt at the
+    next flush after the one that found it off."""
+    g, o = _pair()
+    install(g, edge_world())
+    install(o, edge_world())
+    buf, desc = pack([(f, i) for f, i in edge_frames()[:128]])
+    _check(g, o, buf, desc)
+    st0 = g.table_stats()
+    for s in (g, o):
+        assert s.sock_set(1, _sock(17, 5001)) == 0
+    _check(g, o, buf, desc)
+    st1 = g.table_stats()
+    assert st1["index_rebuilds"] == st0["index_rebuilds"] + 1
+    keys4 = colliding_v4(200)  # past the overflow room: the update turns the index off
+    _install_keys((g, o), keys4, [], first_id=6000)
+    kbuf, kdesc = pack(_world_frames(keys4, []))
+    _check(g, o, kbuf, kdesc)  # (the sock_sets of the install: a rebuild, off)
+    assert g.table_stats()["index_on"] == 0
+    for i, (la, lp) in enumerate(keys4[20:]):
+        for s in (g, o):
+            s.filter_remove(6020 + i, 4, la, lp, None, 0, 17)
+    _check(g, o, kbuf, kdesc)  # incremental flush: finds the index off, asks for a rebuild
+    for s in (g, o):
+        s.filter_remove(6000, 4, keys4[0][0], keys4[0][1], None, 0, 17)
+    _check(g, o, kbuf, kdesc)  # the rebuild
+    st = g.table_stats()
+    assert st["index_on"] == 1, st
+    _check(g, o, buf, desc)
+    g.close()

@@ -61,7 +61,7 @@ for step in ${STEPS:-tests bench}; do
         mkdir -p "$OUT/prof_c$c"
         (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c$c" -o run \
            --output-format csv -- python3 "$ROOT/bench.py" --config "$c" --steps 20 --warmup 5 --steady 0 \
-           --no-cpu-baseline > "$OUT/prof_c$c/bench.log" 2>&1) || fail "prof c$c" $? "$OUT/prof_c$c/bench.log"
+           --no-cpu-baseline ${EXTRA:-} > "$OUT/prof_c$c/bench.log" 2>&1) || fail "prof c$c" $? "$OUT/prof_c$c/bench.log"
         find "$OUT/prof_c$c" -name '*kernel_stats.csv' -exec head -4 {} \;
       done ;;
     hbm)
@@ -70,7 +70,7 @@ for step in ${STEPS:-tests bench}; do
           mkdir -p "$OUT/pmc_c$c/$pass"
           (cd /tmp && timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $pass -d "$OUT/pmc_c$c/$pass" -o run \
              --output-format csv -- python3 "$ROOT/bench.py" --config "$c" --steps 5 --warmup 1 --steady 0 \
-             --no-cpu-baseline > "$OUT/pmc_c$c/$pass.log" 2>&1) || fail "hbm c$c $pass" $? "$OUT/pmc_c$c/$pass.log"
+             --no-cpu-baseline ${EXTRA:-} > "$OUT/pmc_c$c/$pass.log" 2>&1) || fail "hbm c$c $pass" $? "$OUT/pmc_c$c/$pass.log"
         done
         echo "hbm c$c done"
       done ;;
@@ -84,7 +84,7 @@ for step in ${STEPS:-tests bench}; do
         mkdir -p "$OUT/${step}_c$c"
         (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr -d "$OUT/${step}_c$c" -o run \
            --output-format csv -- python3 "$ROOT/bench.py" --config "$c" --steps 3 --warmup 1 --steady 0 \
-           --no-cpu-baseline > "$OUT/${step}_c$c/bench.log" 2>&1) || fail "$step c$c" $? "$OUT/${step}_c$c/bench.log"
+           --no-cpu-baseline ${EXTRA:-} > "$OUT/${step}_c$c/bench.log" 2>&1) || fail "$step c$c" $? "$OUT/${step}_c$c/bench.log"
         echo "$step c$c done"
       done ;;
     ab)
