@@ -24,7 +24,7 @@ CHECK_VARIANTS := r6e4:-DOO_RX_RING=6,-DOO_RX_EXTRA=4 r8e2:-DOO_RX_RING=8,-DOO_R
                   rb12:-DOO_RX_BODY_RING=12
 CHECKS := $(foreach v,$(CHECK_VARIANTS),build/check/liboo_gpu_rx_$(firstword $(subst :, ,$(v))).so)
 
-all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling tools/ring_probe tools/poll_bench $(CHECKS)
+all: $(PRODUCT) $(SHIM) $(PKTGEN) oracle tools/hbm_ceiling tools/ring_probe tools/poll_bench tools/poll_rtt $(CHECKS)
 
 build/check/liboo_gpu_rx_%.so: $(SRCS) $(HDRS)
 	@mkdir -p build/check
@@ -75,6 +75,9 @@ check-integration: oracle
 	  -Iinclude -o build/netif_event_gpu.o integration/netif_event_gpu.c
 
 .PHONY: all oracle asm clean variants check-integration
+
+tools/poll_rtt: tools/poll_rtt.hip
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
 
 tools/hbm_ceiling: tools/hbm_ceiling.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
