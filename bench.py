@@ -173,8 +173,19 @@ def main(argv=None) -> int:
                           "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
                           "cuda_initialized": bool(torch.cuda.is_initialized())}), flush=True)
         return 0
+    _json_only_stdout()
     run_rank(args)
     return 0
+
+
+def _json_only_stdout() -> None:
+    """This rank's file descriptor 1 goes to stderr, so libraries that print
+    to it (librccl writes its version banner there at communicator init) do
+    not mix with the one JSON line, which goes to the original stdout."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(real, "w", buffering=1)
 
 
 def run_rank(args) -> None:
@@ -233,6 +244,7 @@ def run_rank(args) -> None:
             dist.broadcast_object_list(gid, src=0)
         try:
             group = GpuRxGroup.join(local, rank, world, gid[0])
+            log(f"[rank {rank}] joined the library's group ({world} rank(s), librccl)")
         except OSError as e:
             if world == 1:
                 raise
@@ -694,28 +706,46 @@ def time_table_ops(torch, filters, socks, frames, d_desc, n, out, device, reps=5
     g = GpuRxStack(device=device)
     g.load_world(filters, socks)
     g.sync(sh)
-    churn = [f for f in filters if f.af == 4][:50]
 
     def batch():
         g.handle_rx_batch_dev(frames.data_ptr(), frames.numel(), d_desc.data_ptr(), n,
                               out.data_ptr(), 0, sh)
 
-    def churn_and_batch():
-        for f in churn:
+    def churn():
+        for f in churn_f:
             ra = None if f.raddr_any else bytes(f.raddr)[:4]
             g.filter_remove_raw(f.sock, 4, bytes(f.laddr)[:4], f.lport_be, ra, f.rport_be, f.proto)
-        for f in churn:
+        for f in churn_f:
             ra = None if f.raddr_any else bytes(f.raddr)[:4]
             g.filter_insert_raw(f.sock, 4, bytes(f.laddr)[:4], f.lport_be, ra, f.rport_be, f.proto)
+
+    def churn_and_batch():
+        churn()
         batch()
+    churn_f = [f for f in filters if f.af == 4][:50]
     for _ in range(3):
         batch()
     alone = sorted(timed(batch) for _ in range(reps))
+    # (a) as rounds 3-4 measured it: the host calls between the events (the
+    # stream idles while the caller makes them)
     with_churn = sorted(timed(churn_and_batch) for _ in range(reps))
+    # (b) the device's share: the 100 ops queued first (host time reported
+    # apart), then the events around the batch that flushes them
+    dev, host_us = [], []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        churn()
+        host_us.append((time.perf_counter() - t) * 1e6 / (2 * len(churn_f)))
+        dev.append(timed(batch))
+    st = g.table_stats()
     g.close()
     return {"world_ops": len(filters) + len(socks), "world_flush_ms": round(sorted(loads)[reps // 2], 4),
-            "churn_ops": 2 * len(churn), "batch_ms": round(alone[reps // 2], 4),
-            "churn_plus_batch_ms": round(with_churn[reps // 2], 4)}
+            "churn_ops": 2 * len(churn_f), "batch_ms": round(alone[reps // 2], 4),
+            "churn_plus_batch_ms": round(with_churn[reps // 2], 4),
+            "queued_churn_flush_plus_batch_ms": round(sorted(dev)[reps // 2], 4),
+            "host_us_per_op": round(sorted(host_us)[reps // 2], 2),
+            "index_updates": st["index_updates"], "index_rebuilds": st["index_rebuilds"]}
 
 
 def time_host_path(torch, filters, socks, buf, desc, device, batch=1 << 16, reps=3):
