@@ -50,6 +50,8 @@ extern "C" int oo_table_launch_ops(const oo_rx::DevTables* T, const oo_rx::Table
                                    const uint32_t* d_lev_end, uint32_t nlev, uint32_t gen,
                                    uint32_t kx_mode, uint32_t* kx_req, hipStream_t s);
 extern "C" uint32_t oo_table_threads(void);
+extern "C" int oo_launch_len_sample(const void* desc, uint32_t n, uint32_t ring_mask, uint32_t cons,
+                                    uint32_t* out, uint32_t seq, hipStream_t s);
 extern "C" int oo_table_launch_refresh(const oo_rx::DevTables* T, uint32_t gen, hipStream_t s);
 extern "C" int oo_table_launch_init(const oo_rx::DevTables* T, hipStream_t s);
 extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s);
@@ -245,6 +247,19 @@ struct oo_gpu_rx_ctx {
   uint32_t body_tail = 16;     // packets per body_kernel unit at the batch's end
   uint32_t kmode = 0;          // rx kernel: 0 by frame size, 1 always the 4-slot, 2 always the 2-slot
   uint32_t len_hint = 0;       // mean frame length of the batches to come (0: from buffer bytes)
+  // The frame-length profile of the last batch sampled without a hint
+  // (launch(): mixed sizes take the split transform).  A batch whose
+  // descriptors (address, count, ring position) differ from the last sampled
+  // one gets a sample after it (oo_table_kernel.hip len_sample, into host
+  // memory); launches with the same descriptors use it once its event has
+  // completed -- nothing waits for it.
+  uint32_t* h_len = nullptr;
+  uint32_t* d_len = nullptr;
+  hipEvent_t len_ev = nullptr;
+  const void* len_desc = nullptr;
+  uint32_t len_n = 0, len_cons = 0, len_seq = 0;
+  bool len_pending = false;
+  int len_mixed = -1;          // the sampled batch: 1 mixed sizes, 0 not, -1 not known yet
   uint32_t tstep = 8;          // tile size step (KParams::tstep)
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
   // host path
@@ -596,6 +611,8 @@ void free_dev(oo_gpu_rx_ctx* c) {
   if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
   if (c->h_image_hdr) (void)hipHostFree(c->h_image_hdr);
   if (c->h_kx_req) (void)hipHostFree(c->h_kx_req);
+  if (c->h_len) (void)hipHostFree(c->h_len);
+  if (c->len_ev) (void)hipEventDestroy(c->len_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -936,6 +953,9 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
          hipHostGetDevicePointer(reinterpret_cast<void**>(&st.hd), st.h, 0) == hipSuccess &&
          hipMalloc(&st.d, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK) == hipSuccess &&
          hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipHostMalloc(&c->h_len, 128, hipHostMallocDefault) == hipSuccess &&
+       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_len), c->h_len, 0) == hipSuccess &&
+       hipEventCreateWithFlags(&c->len_ev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipHostMalloc(&c->h_kx_req, 128, hipHostMallocDefault) == hipSuccess &&
        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_kx_req), c->h_kx_req, 0) == hipSuccess;
   if (ok) *c->h_kx_req = 0;
@@ -1215,14 +1235,50 @@ static void set_tiles_dyn(KParams& P, uint32_t n, uint64_t W, uint32_t S, uint32
   }
 }
 
+// Whether a launch's batch has the sampled mixed-size profile: the same
+// descriptors (address, count, ring position) as the last sampled batch, and
+// that sample landed.  No caller hint (a hint names the frames' mean size
+// only).
+static bool mixed_sizes(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n) {
+  if (c->len_hint != 0 || c->h_len == nullptr) return false;
+  if (c->len_desc != static_cast<const void*>(P.desc) || c->len_n != n || c->len_cons != P.ring_cons)
+    return false;
+  if (c->len_pending && hipEventQuery(c->len_ev) == hipSuccess) {
+    const volatile uint32_t* h = c->h_len;
+    if (h[6] == c->len_seq) {
+      const double cnt = (double)((uint64_t)h[1] << 32 | h[0]);
+      const double sum = (double)((uint64_t)h[3] << 32 | h[2]);
+      const double sq = (double)((uint64_t)h[5] << 32 | h[4]);
+      c->len_mixed = cnt > 0 && sum >= 1024.0 * cnt && sq * cnt >= 1.36 * sum * sum ? 1 : 0;
+    }
+    c->len_pending = false;
+  }
+  return c->len_mixed == 1;
+}
+
+// After a launch without a hint whose descriptors differ from the last
+// sampled ones: a sample of its lengths on s (best effort: a failure only
+// leaves the profile unknown).
+static void sample_lengths(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n, hipStream_t s) {
+  if (c->len_hint != 0 || c->h_len == nullptr || c->kmode != 0 || n == 0) return;
+  if (c->len_desc == static_cast<const void*>(P.desc) && c->len_n == n && c->len_cons == P.ring_cons)
+    return;
+  c->len_desc = P.desc;
+  c->len_n = n;
+  c->len_cons = P.ring_cons;
+  c->len_mixed = -1;
+  c->len_pending = oo_launch_len_sample(P.desc, n, P.ring_mask, P.ring_cons, c->d_len, ++c->len_seq, s) == 0 &&
+                   hipEventRecord(c->len_ev, s) == hipSuccess;
+}
+
 // The split transform (oo_rx_kernel.hip "The split transform"): win_kernel,
 // then body_kernel, on s.  The stream's pending-word buffer grows in stream
 // order (hipMallocAsync), so no call waits for the device.
 static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Tracked* trk,
-                        uint32_t* set, hipStream_t s, bool short_frames) {
-  // Mixed sizes are the short-frame class's (IMIX): its body engine runs
-  // per-group job sequences, which idle less of the ring on them.
-  const bool gseq = c->body_engine ? c->body_engine == 2 : short_frames;
+                        uint32_t* set, hipStream_t s, bool seq_body) {
+  // Mixed sizes (the short-frame class's IMIX, or a sampled profile): the
+  // body engine runs per-group job sequences, which idle less of the ring.
+  const bool gseq = c->body_engine ? c->body_engine == 2 : seq_body;
   const uint32_t grid_body = gseq ? c->grid_body_gseq : c->grid_body;
   if (trk->pend_n < (uint64_t)n + 64) {
     if (trk->pend != nullptr && hipFreeAsync(trk->pend, s) != hipSuccess) return -EIO;
@@ -1329,12 +1385,22 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // body_kernel finds nothing and returns.  Smaller batches keep one launch.
   const bool window_frames =
       c->len_hint ? c->len_hint <= (uint32_t)oo_rx::HB_BYTES : P.frames_bytes <= (uint64_t)oo_rx::HB_BYTES * n;
-  const bool split = c->kmode == 3 || (c->kmode == 0 && window_frames && n >= (1u << 20));
+  // Mixed frame sizes with long frames among them (the sampled profile:
+  // mean >= 1 KiB, coefficient of variation >= 0.6 -- config 4's IPv4/TCP
+  // 64-9014 B) take the split transform with the sequences body engine:
+  // same-box A/B -2.6 % on config 4, while IMIX (mean 362 B, +6 %) and
+  // uniform frames (config 2, +57 %) keep one launch
+  // (profiles/r05/ab_split_c4_c5.log).
+  const bool mixed = !tx && c->kmode == 0 && mixed_sizes(c, P, n);
+  const bool split = c->kmode == 3 || (c->kmode == 0 && ((window_frames && n >= (1u << 20)) ||
+                                                        (mixed && n >= (1u << 16))));
   if (!tx && split && split_fits && c->grid_win > 0 && c->grid_body > 0 && c->grid_body_gseq > 0) {
-    const int rc = launch_split(c, P, n, trk, P.claim, s, short_frames);  // (flips the parity)
+    const bool seq_body = short_frames || mixed;
+    const int rc = launch_split(c, P, n, trk, P.claim, s, seq_body);  // (flips the parity)
     if (rc != 0) return rc;
-    c->last_path = (c->body_engine ? c->body_engine == 2 : short_frames) ? 4u : 3u;
+    c->last_path = (c->body_engine ? c->body_engine == 2 : seq_body) ? 4u : 3u;
     note_launch(trk);
+    sample_lengths(c, P, n, s);
     return 0;
   }
   const bool use_short = !tx && c->grid_short > 0 && (c->kmode == 2 || (c->kmode == 0 && short_frames));
@@ -1377,6 +1443,7 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   if (!tx) {
     note_launch(trk);
     c->last_path = use_short ? 2u : 1u;
+    sample_lengths(c, P, n, s);
   }
   return 0;
 }

@@ -74,9 +74,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef OO_RX_GSEQ
 #define OO_RX_GSEQ 0  // 1: per-group job sequences instead of lockstep job slots
 #endif
-#ifndef OO_RX_LLCS
-#define OO_RX_LLCS 0  // 1: rx_kernel streams a tile's bodies as one line stream (below)
-#endif
 
 constexpr int WAVES = OO_RX_WAVES;
 constexpr int R = OO_RX_RING;
@@ -133,14 +130,6 @@ __device__ __forceinline__ void lds_read16x2(const void* p0, const void* p1, uin
                : "=&v"(v0), "=&v"(v1)
                : "v"((uint32_t)(uintptr_t)(lptr)(p0)), "v"((uint32_t)(uintptr_t)(lptr)(p1))
                : "memory");
-}
-
-// LDS write / add of one word the compiler cannot see (as lds_read16).
-__device__ __forceinline__ void lds_write4_(void* p, uint32_t v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_add4_(void* p, uint32_t v) {
-  asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)(lptr)(p)), "v"(v) : "memory");
 }
 
 // Value of v in lane src (ds_bpermute: no LDS memory access, so it needs no
@@ -1975,162 +1964,6 @@ __device__ __forceinline__ void consume_round(ConsumeCursor& c, const Jobs& J, c
 
 #endif  // OO_RX_GSEQ
 
-// ---------------------------------------------------------------------------
-// The line stream (OO_RX_LLCS, rx_kernel only).  A tile's bodies are laid end
-// to end as one stream of 128-B lines -- job j's lines [lp_j, lp_j + nl_j),
-// jobs in lane (buffer) order -- and round r reads lines 8r .. 8r + 7, one per
-// 8-lane group.  Every round but the tile's last carries eight body lines
-// whatever the frame sizes (job slots idle the lanes of shorter jobs: config 4
-// carries 142 rounds per tile for 111 rounds of lines), and a
-// job change costs a compare against a scalar boundary instead of the job's
-// fields fetched and masks rebuilt.  A line's owner is the last job whose
-// first line is at or before it: jr, the owner of the round's first line, is
-// wave-uniform, and the boundaries inside the round (at most eight, usually
-// one or two) are read as scalars.  Each group's line sum goes into the job's
-// LDS total with one LDS add; the packet's lane reads its total at the end.
-// Lanes past a job's last chunk re-read that chunk (the same line) with
-// weight 0, as the slot engines do.
-
-struct LJobs {
-  uint32_t a0c;   // lane j < M: job j's a0 as a chunk index from fbase (a0 = fbase + 16 a0c)
-  uint32_t lpl;   // lane j < M: lp_j | lim_j << 16 (first line; frame end relative to a0);
-                  // lanes >= M: NL
-  uint64_t fbase;  // the frame buffer's 16-B-aligned start (wave-uniform)
-  uint32_t M, NL;  // jobs, lines (wave-uniform)
-  uint32_t T;      // rounds
-};
-
-struct LCursor {
-  uint32_t r, jr;  // round, owner of its first line (wave-uniform)
-};
-typedef LCursor LIssue;
-typedef LCursor LConsume;
-
-// Inclusive prefix sum over the wave's lanes: within each row of 16 lanes
-// (row_shr 1, 2, 4, 8), then row ends broadcast into the rows after them
-// (row_bcast 15, 31) -- DPP only: no per-lane address registers.  All lanes
-// active.
-__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return v;
-}
-
-// The tile's jobs; myslot = this packet's job (64: none).  jsum: the wave's
-// 64 LDS totals, zeroed here.  fbase: the frame buffer's 16-B-aligned start
-// (the host takes this engine only for buffers under 64 GiB: a0c is 32
-// bits).  All lanes active.
-__device__ __forceinline__ LJobs ljobs_setup(uint64_t abase, int span, uint32_t lane,
-                                             uint32_t& myslot, uint32_t* jsum, uint64_t fbase) {
-  const uint32_t off0 = body_off0(abase);
-  const uint32_t nb = body_chunks(off0, span);
-  const uint64_t bm = __ballot(nb != 0);
-  LJobs J;
-  lds_write4_(&jsum[lane], 0u);
-  J.fbase = fbase;
-  if (bm == 0) {
-    myslot = 64u;
-    J.a0c = J.lpl = 0;
-    J.M = J.NL = J.T = 0;
-    return J;
-  }
-  const uint32_t M = (uint32_t)__popcll(bm);
-  const uint32_t below =
-      __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-  const uint32_t j = nb != 0 ? below : M + lane - below;  // a permutation of 0..63
-  const uint32_t nl = (nb + 7u) >> 3;
-  const uint32_t incl = wave_scan_incl(nl);
-  const uint32_t NL = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  auto push = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_permute((int)(j << 2), (int)v); };
-  J.a0c = push((uint32_t)((abase + off0 - fbase) >> 4));
-  J.lpl = push(nb != 0 ? (incl - nl) | (((uint32_t)span - off0) << 16) : NL);
-  J.M = M;
-  J.NL = NL;
-  J.T = (NL + 7u) >> 3;
-  myslot = nb != 0 ? j : 64u;
-  return J;
-}
-
-// The owner of this lane's line L of round c.r (an offset from c.jr), and the
-// owner of the next round's first line.
-__device__ __forceinline__ uint32_t lowner(const LCursor& c, const LJobs& J, uint32_t L,
-                                           uint32_t& njr) {
-  const uint32_t end = 8u * c.r + 8u;
-  uint32_t off = 0, k = c.jr + 1u, bk = 0;
-  while (k < J.M) {
-    bk = (uint32_t)__builtin_amdgcn_readlane((int)J.lpl, (int)k) & 0xffffu;
-    if (bk >= end) break;
-    off += L >= bk ? 1u : 0u;
-    ++k;
-  }
-  njr = (k < J.M && bk == end) ? k : k - 1u;
-  return c.jr + off;
-}
-
-__device__ __forceinline__ void lissue_start(LIssue& c) {
-  c.r = 0;
-  c.jr = 0;
-}
-
-__device__ __forceinline__ void issue_round(LIssue& c, const LJobs& J, uint64_t zero, void* slot,
-                                            uint32_t lane) {
-  const uint32_t L = 8u * c.r + (lane >> 3);
-  uint32_t njr;
-  const uint32_t o = lowner(c, J, L, njr);
-  const uint32_t a0c = lane_get(J.a0c, o), lpl = lane_get(J.lpl, o);
-  const uint32_t nb = ((lpl >> 16) + 15u) >> 4;
-  const uint32_t ci = 8u * (L - (lpl & 0xffffu)) + (lane & 7u);
-  const uint64_t a = J.fbase + 16ull * (uint64_t)(a0c + min(ci, nb - 1u));
-  glds<OO_RX_BODY_AUX>(L < J.NL ? a : zero, slot);
-  ++c.r;
-  c.jr = njr;
-}
-
-__device__ __forceinline__ void lconsume_start(LConsume& c) {
-  c.r = 0;
-  c.jr = 0;
-}
-
-__device__ __forceinline__ void consume_round(LConsume& c, const LJobs& J, const uint4& v,
-                                              uint32_t lane, uint32_t* jsum) {
-  const uint32_t L = 8u * c.r + (lane >> 3);
-  uint32_t njr;
-  const uint32_t o = lowner(c, J, L, njr);
-  const uint32_t lpl = lane_get(J.lpl, o);
-  const uint32_t lim = lpl >> 16;
-  const uint32_t cb = 16u * (8u * (L - (lpl & 0xffffu)) + (lane & 7u));  // chunk's first byte
-  const bool line = L < J.NL;
-  const bool live = line && cb < lim;
-  const uint32_t vb = live ? min(lim - cb, 16u) : 0u;
-  uint32_t s;
-  if (__ballot(live && vb != 16u) == 0) {
-    const uint32_t w = live ? 0x00010001u : 0u;
-    uint32_t a = dot(v.x, w, 0u);
-    uint32_t b = dot(v.y, w, 0u);
-    a = dot(v.z, w, a);
-    b = dot(v.w, w, b);
-    s = a + b;
-  } else {  // a frame's partial last chunk (an odd end: the last word's high byte is 0)
-    auto bytes = [](int k) -> uint32_t {
-      return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * k)) - 1u;
-    };
-    const int n = (int)vb;
-    uint32_t a = dot(v.x & bytes(n), 0x00010001u, 0u);
-    uint32_t b = dot(v.y & bytes(n - 4), 0x00010001u, 0u);
-    a = dot(v.z & bytes(n - 8), 0x00010001u, a);
-    b = dot(v.w & bytes(n - 12), 0x00010001u, b);
-    s = a + b;
-  }
-  const uint32_t t = group_sum8(s);
-  if ((lane & 7u) == 0u && line) lds_add4_(&jsum[o], t);
-  ++c.r;
-  c.jr = njr;
-}
-
 // Tiles.  The batch is cut into P.ntiles tiles, K per tile-processing wave
 // (rx_kernel's waves), which take tiles w, w + W, ...
 // (all waves sweep the buffer together: reading one ~200-MB window at a time
@@ -2537,9 +2370,6 @@ struct WaveLds {
   uint32_t cnt[OO_RX_R_COUNT];  // per-reason counts
   uint32_t dbase, gofs;          // claims: first dynamic tile of the group, counter offset
   uint32_t T0, pad;              // the tile's body rounds (kept out of the registers)
-#if OO_RX_LLCS
-  uint32_t jsum[64];             // the line stream's job totals
-#endif
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "WaveLds is carved from a uint4 array");
 constexpr int WAVE_U4 = (int)(sizeof(WaveLds) / 16);
@@ -2691,23 +2521,13 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // rows are consumed.  T: the ring-loop rounds (a multiple of R; the
     // padding rounds read zeros).
     uint32_t myslot;
-#if OO_RX_LLCS
-    const LJobs J = ljobs_setup(dv.abase, dv.span, lane, myslot, L.jsum,
-                                sreg64(P.frames) & ~(uint64_t)15);
-#else
     const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot);
-#endif
     uint32_t T0 = J.T;
     bool ext = E > 0 && T0 > (uint32_t)(R + E);
     uint32_t T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
     if (lane == 0) lds_write4(&L.T0, T0);
-#if OO_RX_LLCS
-    LIssue ci;
-    lissue_start(ci);
-#else
     IssueCursor ci;
     if (T0 != 0) issue_slot(ci, J, 0, lane, zero);  // (body-less tiles issue no rounds)
-#endif
     // This tile's header windows: older than the previous tile's NST stores
     // (none before the first tile) and the R rounds issued here.
     if (T != 0) {
@@ -2786,11 +2606,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 
     // The consume side's cursor is set up only now: its registers are free
     // during the header work, where the demux loads need them.
-#if OO_RX_LLCS
-    LConsume cc;
-    lconsume_start(cc);
-#define OO_CONSUME(v) consume_round(cc, J, v, lane, L.jsum)
-#else
     ConsumeCursor cc;
     if (T0 != 0) {
       consume_start(cc, J, lane);
@@ -2798,8 +2613,6 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       cc.acc = 0;
       cc.bs = 0;
     }
-#define OO_CONSUME(v) consume_round(cc, J, v, lane)
-#endif
 
     // ---- body stream, two pieces per step.  Each wait counts the
     // operations issued after the awaited pair (the demux loads excepted:
@@ -2813,8 +2626,8 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
         vm_wait<R + E>();
         uint4 v0, v1;
         lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
-        OO_CONSUME(v0);
-        OO_CONSUME(v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
         issue_round(ci, J, zero, &L.ring[u][0], lane);
         issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
       }
@@ -2825,8 +2638,8 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
         vm_wait_n(R + E - u);
         uint4 v0, v1;
         lds_read16x2(&L.hdr[u][lane], &L.hdr[u + 1][lane], v0, v1);
-        OO_CONSUME(v0);
-        OO_CONSUME(v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
       }
       stage_next();
     }
@@ -2844,8 +2657,8 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
         else vm_wait<R - 2>();
         uint4 v0, v1;
         lds_read16x2(&L.ring[u][lane], &L.ring[u + 1][lane], v0, v1);
-        OO_CONSUME(v0);
-        OO_CONSUME(v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
         if (!last) {
           issue_round(ci, J, zero, &L.ring[u][0], lane);
           issue_round(ci, J, zero, &L.ring[u + 1][0], lane);
@@ -2860,12 +2673,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     }
     STAMP(4, __builtin_amdgcn_s_memrealtime());
 
-#undef OO_CONSUME
-#if OO_RX_LLCS
-    const uint32_t body = myslot < 64u ? lds_read4(&L.jsum[myslot]) : 0u;
-#else
     const uint32_t body = lane_get(cc.bs, myslot);
-#endif
     if constexpr (TX) {
       store_checks(P, dv, th, tx_l4_check(th, dv.shift, body), lane, L.ring);
     } else {

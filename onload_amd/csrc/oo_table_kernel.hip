@@ -611,6 +611,36 @@ __global__ __launch_bounds__(TABLE_THREADS) void table_ops(DevTables T, const Ta
   }
 }
 
+// ---------------------------------------------------------------------------
+// A batch's frame-length profile for the launch choice (oo_gpu_rx.cpp
+// launch(): mixed sizes take the split transform): 256 descriptors evenly
+// spaced over the batch (plain or AF_XDP ring entries: the length is the
+// 16-bit field at byte 8 in both), their count, sum and sum of squares, stored
+// to host memory with the sequence number last (the host reads it once the
+// launch's event has completed).
+__global__ __launch_bounds__(256) void len_sample(const uint8_t* desc, uint32_t n, uint32_t ring_mask,
+                                                  uint32_t cons, uint32_t* out, uint32_t seq) {
+  __shared__ uint64_t acc[3];
+  const uint32_t t = threadIdx.x;
+  if (t < 3u) acc[t] = 0;
+  __syncthreads();
+  if (n != 0 && (n >= 256u || t < n)) {
+    const uint32_t i = n >= 256u ? (uint32_t)(((uint64_t)t * n) >> 8) : t;
+    const uint32_t len = *reinterpret_cast<const uint16_t*>(desc + 16ull * ((cons + i) & ring_mask) + 8u);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&acc[0]), 1ull);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&acc[1]), (unsigned long long)len);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&acc[2]), (unsigned long long)len * len);
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int k = 0; k < 3; ++k) {
+      out[2 * k] = (uint32_t)acc[k];
+      out[2 * k + 1] = (uint32_t)(acc[k] >> 32);
+    }
+    __hip_atomic_store(out + 6, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace oo_rx
 
 namespace {
@@ -669,5 +699,14 @@ extern "C" int oo_table_launch_kx(const oo_rx::DevTables* T, hipStream_t s) {
 extern "C" int oo_table_launch_occ(const oo_rx::DevTables* T, hipStream_t s) {
   hipLaunchKernelGGL(oo_rx::table_occ, dim3(grid_for((T->ip4_mask + T->ip6_mask + 2u) / 32u + 2u)),
                      dim3(256), 0, s, *T);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The frame-length sample of a batch into host memory `out` (7 words: count,
+// sum, sum of squares as u64 pairs, then seq), on s after the batch.
+extern "C" int oo_launch_len_sample(const void* desc, uint32_t n, uint32_t ring_mask, uint32_t cons,
+                                    uint32_t* out, uint32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(oo_rx::len_sample, dim3(1), dim3(256), 0, s,
+                     static_cast<const uint8_t*>(desc), n, ring_mask, cons, out, seq);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
