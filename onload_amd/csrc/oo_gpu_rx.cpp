@@ -24,6 +24,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <new>
 #include <unordered_map>
 #include <unordered_set>
@@ -118,6 +120,7 @@ static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
 #define OO_KX_V6_MUL 4  // IPv6 index entries per table slot
 #endif
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
+constexpr uint32_t SMALL_N = 2048;    // launch(): batches up to this many packets take 8-packet tiles
 constexpr int NTRACK = 8;             // streams tracked at once (LRU)
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
 // Tile-claim counter sets: two per tracked stream (its launches alternate
@@ -169,6 +172,8 @@ struct HostSlot {
   oo_gpu_pkt_desc* h_desc = nullptr;
   oo_gpu_rx_result* h_out = nullptr;
   uint32_t* h_ctr = nullptr;
+  uint32_t* h_done = nullptr;  // pinned: the slot's last completed ticket (low 32 bits),
+  uint32_t* d_done = nullptr;  //   written by the stream after the batch (complete_slot spins on it)
   bool busy = false;
   uint64_t ticket = 0;
   uint32_t n = 0;
@@ -598,7 +603,7 @@ void free_dev(oo_gpu_rx_ctx* c) {
   for (HostSlot& s : c->slot) {
     for (void* p : {(void*)s.d_frames, (void*)s.d_desc, (void*)s.d_out, (void*)s.d_ctr})
       if (p) (void)hipFree(p);
-    for (void* p : {(void*)s.h_frames, (void*)s.h_desc, (void*)s.h_out, (void*)s.h_ctr})
+    for (void* p : {(void*)s.h_frames, (void*)s.h_desc, (void*)s.h_out, (void*)s.h_ctr, (void*)s.h_done})
       if (p) (void)hipHostFree(p);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -822,8 +827,11 @@ int alloc_host_slots(oo_gpu_rx_ctx* c) {
         hipHostMalloc(&s.h_frames, c->stage_bytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&s.h_desc, sizeof(oo_gpu_pkt_desc) * pk, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&s.h_out, sizeof(oo_gpu_rx_result) * pk, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&s.h_ctr, sizeof(oo_gpu_rx_counters), hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc(&s.h_ctr, sizeof(oo_gpu_rx_counters), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.h_done, 128, hipHostMallocDefault) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_done), s.h_done, 0) != hipSuccess)
       return -ENOMEM;
+    *s.h_done = 0;
   }
   return 0;
 }
@@ -1260,7 +1268,9 @@ static bool mixed_sizes(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n) {
 // sampled ones: a sample of its lengths on s (best effort: a failure only
 // leaves the profile unknown).
 static void sample_lengths(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n, hipStream_t s) {
-  if (c->len_hint != 0 || c->h_len == nullptr || c->kmode != 0 || n == 0) return;
+  // (only batches the profile can change the choice of: a poll's small
+  // batches would pay a launch for nothing)
+  if (c->len_hint != 0 || c->h_len == nullptr || c->kmode != 0 || n < (1u << 16)) return;
   if (c->len_desc == static_cast<const void*>(P.desc) && c->len_n == n && c->len_cons == P.ring_cons)
     return;
   c->len_desc = P.desc;
@@ -1405,7 +1415,13 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   }
   const bool use_short = !tx && c->grid_short > 0 && (c->kmode == 2 || (c->kmode == 0 && short_frames));
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
-  const uint32_t need = (n + 63) / 64;  // waves if every tile were full
+  // A small batch (a poll's worth: at most SMALL_N packets) is cut into tiles
+  // of 8 packets, a wave each, statically: its bodies stream in parallel, so
+  // the batch takes about one tile's latency -- over PCIe (frames read in
+  // place from host memory) one 64-packet tile's 12 KiB in flight would take
+  // many round trips.  Larger batches: full 64-packet tiles.
+  const bool small = n <= SMALL_N;
+  const uint32_t need = small ? (n + 7) / 8 : (n + 63) / 64;  // waves, a tile each
   const uint32_t blocks = std::max<uint32_t>(
       1, std::min<uint32_t>((need + wpb - 1) / wpb, use_short ? c->grid_short : c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
@@ -1416,8 +1432,8 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
   // single waves (same-box A/B).
   set_groups(P, W, c->ngroups_max ? c->ngroups_max : (short_frames ? 32u : CLAIM_GROUPS),
              c->gshift != ~0u ? c->gshift : (short_frames ? 4u : 0u));
-  P.dyn = c->dyn ? 1u : 0u;
-  if (c->dyn) {
+  P.dyn = c->dyn && !small ? 1u : 0u;
+  if (P.dyn) {
     set_tiles_dyn(P, n, W, c->tail_tile, c->tail_per_wave);
   } else {
     // Static balanced partition: the W waves each take K = ceil(n / (64 W))
@@ -1559,8 +1575,32 @@ int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
   return -ENOENT;
 }
 
+// The slot's done word: written by the stream after everything the batch
+// enqueued (hipStreamWriteValue32), so seeing it means the records and
+// counters have landed.  The waiting thread spins on it -- a host read of its
+// own memory, no runtime call -- for up to kSpinNs, then waits on the
+// slot's event (a stream that failed to write it, or a long batch).
+constexpr int64_t kSpinNs = 50 * 1000 * 1000;
+static uint32_t done_word(uint64_t ticket) { return ((uint32_t)ticket & 0x7fffffffu) + 1u; }  // never 0
+static bool spin_done(const HostSlot& s) {
+  if (s.h_done == nullptr) return false;
+  const uint32_t want = done_word(s.ticket);
+  const volatile uint32_t* w = s.h_done;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
+    if (*w == want) {
+      std::atomic_thread_fence(std::memory_order_acquire);
+      return true;
+    }
+    if ((i & 1023u) == 1023u &&
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                .count() > kSpinNs)
+      return false;
+  }
+}
+
 static int complete_slot(oo_gpu_rx_ctx* c, HostSlot& s) {
-  if (hipEventSynchronize(s.done) != hipSuccess) {
+  if (!spin_done(s) && hipEventSynchronize(s.done) != hipSuccess) {
     s.busy = false;
     return -EIO;
   }
@@ -1616,6 +1656,7 @@ int oo_gpu_rx_submit(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes
   }
   ok = ok && hipMemcpyAsync(s.h_ctr, s.d_ctr, sizeof(oo_gpu_rx_counters), hipMemcpyDeviceToHost,
                             st) == hipSuccess &&
+       hipStreamWriteValue32(st, s.d_done, done_word(t), 0) == hipSuccess &&
        hipEventRecord(s.done, st) == hipSuccess;
   if (!ok) return -EIO;
   s.busy = true;
@@ -1649,7 +1690,9 @@ int oo_gpu_rx_submit_mapped(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t fra
     if (rc == 0) rc = launch(c, d_frames, frames_bytes, d_desc, n, d_out, nullptr, st);
     if (rc) return rc;
   }
-  if (hipEventRecord(s.done, st) != hipSuccess) return -EIO;
+  if (hipStreamWriteValue32(st, s.d_done, done_word(t), 0) != hipSuccess ||
+      hipEventRecord(s.done, st) != hipSuccess)
+    return -EIO;
   s.busy = true;
   s.ticket = t;
   s.n = n;

@@ -336,18 +336,19 @@ static void dispatch(oo_rx_poll* p, uint32_t id, const uint8_t* frame,
 /* The crossover's cost model (oo_rx_poll.h): whether the device batch of m
  * frames and `bytes` frame bytes costs less than the caller's per-event
  * path.  The defaults are tools/poll_bench's fits on MI355X boxes
- * (DESIGN.md §5e): the per-event path 20.3 ns per frame + 0.146 ns per byte
- * on one host core; a device batch ~30 us fixed (launches, completion,
- * PCIe latency) + 15.2 ns per frame, + 0.029 ns per byte read in place
- * (zero copy) or 0.081 ns per byte gathered (the host memcpy). */
+ * (DESIGN.md §5e, round 5): the per-event path 20.3 ns per frame + 0.146 ns
+ * per byte on one host core; a device batch ~18.5 us fixed (launch, PCIe
+ * round trips, the completion word) + 15 ns per frame, + 0.023 ns per byte
+ * read in place (zero copy) or 0.081 ns per byte gathered (the host
+ * memcpy). */
 static int gpu_pays(const oo_rx_poll* p, uint64_t m, uint64_t bytes)
 {
   const oo_rx_poll_cfg* c = &p->cfg;
   const uint64_t cpu_pkt = c->cpu_pkt_ps ? c->cpu_pkt_ps : 20300;
   const uint64_t cpu_byte = c->cpu_byte_ps ? c->cpu_byte_ps : 146;
-  const uint64_t fixed = (uint64_t)(c->gpu_fixed_ns ? c->gpu_fixed_ns : 30000) * 1000u;
-  const uint64_t gpu_pkt = c->gpu_pkt_ps ? c->gpu_pkt_ps : 15200;
-  const uint64_t gpu_byte = c->gpu_byte_ps ? c->gpu_byte_ps : (p->zero_copy ? 29 : 81);
+  const uint64_t fixed = (uint64_t)(c->gpu_fixed_ns ? c->gpu_fixed_ns : 18500) * 1000u;
+  const uint64_t gpu_pkt = c->gpu_pkt_ps ? c->gpu_pkt_ps : 15000;
+  const uint64_t gpu_byte = c->gpu_byte_ps ? c->gpu_byte_ps : (p->zero_copy ? 23 : 81);
   return fixed + m * gpu_pkt + bytes * gpu_byte < m * cpu_pkt + bytes * cpu_byte;
 }
 
@@ -428,10 +429,16 @@ static int chunk_submit(oo_rx_poll* p, struct chunk* c, const oo_rx_poll_ev* evs
                                  c->d_rec, &c->ticket);
     (void)oo_gpu_rx_set_len_hint(p->gpu, 0);
   }
-  else if( p->mapped )
-    rc = oo_gpu_rx_submit_mapped(p->gpu, c->d_pack, at, c->d_desc, m, c->d_rec, &c->ticket);
-  else
-    rc = oo_gpu_rx_submit(p->gpu, c->pack, at, c->desc, m, c->rec, NULL, &c->ticket);
+  else {
+    /* the gathered frames are packed, but their mean length names the
+     * kernel instance without a look at the buffer */
+    (void)oo_gpu_rx_set_len_hint(p->gpu, (uint32_t)(total / m) ? (uint32_t)(total / m) : 1u);
+    if( p->mapped )
+      rc = oo_gpu_rx_submit_mapped(p->gpu, c->d_pack, at, c->d_desc, m, c->d_rec, &c->ticket);
+    else
+      rc = oo_gpu_rx_submit(p->gpu, c->pack, at, c->desc, m, c->rec, NULL, &c->ticket);
+    (void)oo_gpu_rx_set_len_hint(p->gpu, 0);
+  }
   if( rc < 0 )
     return rc;
   c->busy = 1;

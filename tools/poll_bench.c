@@ -86,6 +86,10 @@ int main(int argc, char** argv)
     fprintf(stderr, "usage: %s config frames evs_per_poll...\n", argv[0]);
     return 2;
   }
+  /* the process setting INTEGRATION.md §6 recommends for the context's owner
+   * (kernel arguments read from HBM, not over PCIe), before the runtime
+   * starts; an explicit value in the environment wins */
+  setenv("HIP_FORCE_DEV_KERNARG", "1", 0);
   cfg = atoi(argv[1]);
   n = atoi(argv[2]);
   filters = calloc(8192, sizeof(*filters));
