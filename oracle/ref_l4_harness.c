@@ -63,9 +63,12 @@
 #include "netif_event.c"                  /* -I src/lib/transport/ip */
 #include "udp_internal.h"
 
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 static ci_netif ni_;
 static ci_netif* ni = &ni_;
@@ -73,7 +76,7 @@ static int nsocks_;
 
 /* ---- the record of one frame */
 static struct {
-  int kernel, entry, l4off, ip_paylen, stage, fut;
+  int kernel, entry, l4off, ip_paylen, stage, fut, tso;
   int n[3], first[3];
   unsigned hash;
 } R;
@@ -114,6 +117,88 @@ static int sock_id(ci_sock_cmn* s)
   return (int) OO_SP_TO_INT(oo_statep_to_sockp(ni, (oo_p) ((char*) s - (char*) ni->state)));
 }
 
+/* ---- the TCP timestamp-option fast layout (OO_RX_F_TSO), observed on the
+ * reference's own code: ci_tcp_rx_deliver_to_conn (tcp_rx.c:4534-4546) takes
+ * the layout test before anything that needs an established connection.  The
+ * real callback runs on the stage-1 match in a forked child (its socket and
+ * the stack are this process's copies, thrown away), with the rx packet's
+ * timestamps preset to sentinels: the fast layout writes them and sets
+ * CI_TCPT_FLAG_TSO; any other layout calls ci_tcp_parse_options (wrapped
+ * here: reported at once).  Whatever the callback does after the test -- it
+ * runs on a socket the harness never connected, so it may trap or fault --
+ * ends the child and is reported from its signal handler.  1 / 0: the layout
+ * test's outcome; -1: the child ended before reaching it; -2: not probed. */
+#define PROBE_TS1 0xa5c3e1f7u
+#define PROBE_TS2 0x5a3c1e7fu
+static int g_probe_fd = -1, g_probe_slow;
+static ciip_tcp_rx_pkt* g_probe_rxp;
+
+static int probe_state(void)
+{
+  if( g_probe_slow )
+    return 0;
+  if( g_probe_rxp->timestamp != PROBE_TS1 || g_probe_rxp->timestamp_echo != PROBE_TS2 )
+    return (g_probe_rxp->flags & CI_TCPT_FLAG_TSO) ? 1 : 0;
+  return -1;
+}
+
+static void probe_report(int v)
+{
+  char ch = (char) ('0' + v + 1);
+  ssize_t rc = write(g_probe_fd, &ch, 1);
+  (void) rc;
+  _exit(0);
+}
+
+static void probe_sig(int sig)
+{
+  (void) sig;
+  probe_report(probe_state());
+}
+
+extern int __real_ci_tcp_parse_options(ci_netif*, ciip_tcp_rx_pkt*, ci_tcp_options*);
+int __wrap_ci_tcp_parse_options(ci_netif* n, ciip_tcp_rx_pkt* rxp, ci_tcp_options* o)
+{
+  if( g_probe_fd >= 0 ) {
+    g_probe_slow = 1;
+    probe_report(0);
+  }
+  return __real_ci_tcp_parse_options(n, rxp, o);
+}
+
+static int tso_probe(ci_sock_cmn* s, int (*cb)(ci_sock_cmn*, void*), void* arg)
+{
+  int fds[2], v = -1;
+  char ch;
+  pid_t pid;
+  if( pipe(fds) != 0 )
+    return -1;
+  fflush(stdout);
+  pid = fork();
+  if( pid == 0 ) {
+    static const int sigs[] = { SIGSEGV, SIGBUS, SIGILL, SIGTRAP, SIGFPE, SIGABRT, SIGALRM };
+    unsigned k;
+    close(fds[0]);
+    g_probe_fd = fds[1];
+    g_probe_rxp = arg;
+    for( k = 0; k < sizeof(sigs) / sizeof(sigs[0]); ++k )
+      signal(sigs[k], probe_sig);
+    alarm(2);
+    g_probe_rxp->timestamp = PROBE_TS1;
+    g_probe_rxp->timestamp_echo = PROBE_TS2;
+    g_probe_rxp->flags = 0;
+    (void) cb(s, arg);
+    probe_report(probe_state());
+  }
+  close(fds[1]);
+  if( pid > 0 && read(fds[0], &ch, 1) == 1 )
+    v = ch - '0' - 1;
+  close(fds[0]);
+  if( pid > 0 )
+    waitpid(pid, NULL, 0);
+  return v;
+}
+
 /* ---- observed lookups */
 struct count { int n; int first; };
 
@@ -125,9 +210,13 @@ static int count_cb(ci_sock_cmn* s, void* arg)
   return 0;
 }
 
-static int stage_done(unsigned proto, struct count* c, void* arg)
+static int stage_done(unsigned proto, struct count* c, void* arg,
+                      int (*cb)(ci_sock_cmn*, void*))
 {
-  int k = R.stage++;
+  int k = R.stage;
+  if( k == 0 && proto == IPPROTO_TCP && c->n > 0 && cb == ci_tcp_rx_deliver_to_conn )
+    R.tso = tso_probe(ID_TO_SOCK(ni, c->first), cb, arg);
+  ++R.stage;
   if( k < 3 ) {
     R.n[k] = c->n;
     R.first[k] = c->first;
@@ -163,7 +252,7 @@ int __wrap_ci_netif_filter_for_each_match(ci_netif* n, unsigned la, unsigned lp,
     if( R.stage == 0 )
       R.hash = h;
   }
-  return stage_done(proto, &c, arg);
+  return stage_done(proto, &c, arg, cb);
 }
 
 #if CI_CFG_IPV6
@@ -189,7 +278,7 @@ int __wrap_ci_netif_filter_for_each_match_ip6(ci_netif* n, const ci_addr_t* la, 
     if( R.stage == 0 )
       R.hash = h;
   }
-  return stage_done(proto, &c, arg);
+  return stage_done(proto, &c, arg, cb);
 }
 #endif
 
@@ -434,6 +523,7 @@ static void do_frame(int intf, const char* hex)
   for( i = 0; i < 3; ++i )
     R.n[i] = R.first[i] = -1;
   R.fut = -2;
+  R.tso = -2;
   g_ipcsum = 0;
   g_udpcsum = g_tcpcsum = -1;
   stats_save(&g_ip0, &g_ni0);
@@ -443,9 +533,9 @@ static void do_frame(int intf, const char* hex)
   ipcsum = g_ipcsum;
   udpc = g_udpcsum;
   tcpc = g_tcpcsum;
-  printf("r %d %d %d %d %d %d %d %d %d %d %d %u %d", handled, R.kernel, R.entry, R.l4off,
+  printf("r %d %d %d %d %d %d %d %d %d %d %d %u %d %d", handled, R.kernel, R.entry, R.l4off,
          R.ip_paylen, R.n[0], R.first[0], R.n[1], R.first[1], R.n[2], R.first[2], R.hash,
-         R.fut);
+         R.fut, R.tso);
   /* Run 2 (IS_IP6 clear), a dropped frame only (no handler runs): which
    * address-family branch wrote the flag.  Its counters are undone. */
   if( ! handled ) {

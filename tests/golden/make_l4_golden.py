@@ -10,7 +10,10 @@ stores what the reference answered for every frame:
 
   <corpus>/out     int64 (n, 14): handled, kernel, entry (0 / 6 / 17), l4off,
                    ip_paylen, n1, first1, n2, first2, n3, first3, hash (TCP
-                   stage 1), fut (pre-future socket; -1 none, -2 not run)
+                   stage 1), fut (pre-future socket; -1 none, -2 not run),
+                   tso (the timestamp-option fast layout test of
+                   ci_tcp_rx_deliver_to_conn on the stage-1 match: 1 / 0,
+                   -1 not reached, -2 not probed)
                    -- columns as tests/l4_ref.py names them
   <corpus>/obs     int64 (n, 6): what tells handle_rx_csum_bad's drop
                    branches apart -- eth, ipcsum, udp, udpset, tcp, proto

@@ -18,6 +18,10 @@ What the reference's run pins, per frame:
             IP4_OPTS_BAD, TCP_SCATTERED);
   fut       the socket ci_udp_handle_rx_pre_future / ci_tcp_handle_rx_pre_
             future resolve (udp_internal.h:41-103, tcp_rx.h:150-184; IPv4);
+  tso       the TCP timestamp-option fast layout (OO_RX_F_TSO):
+            ci_tcp_rx_deliver_to_conn's own layout test (tcp_rx.c:4534-4546),
+            run on the stage-1 match in a forked child of the harness (1 / 0;
+            -1 the child ended before the test; -2 not a TCP stage-1 match);
   obs       which of handle_rx_csum_bad's drop branches a dropped frame took
             (netif_event.c:1024-1127), from what the run shows: the
             address-family branch that ran, which checksum functions ran and
@@ -39,7 +43,7 @@ from onload_amd import _abi
 from onload_amd.rx import htons
 
 COLS = ("handled", "kernel", "entry", "l4off", "ip_paylen", "n1", "f1", "n2", "f2", "n3", "f3",
-        "hash", "fut")
+        "hash", "fut", "tso")
 HWPORTS = (0, 1, 3, 2, 5)
 CORPORA = ("edge", "edge99", "c2", "c3", "c4", "c5")
 CONFIG_SAMPLE = 3000  # frames per configuration sample
@@ -258,6 +262,10 @@ def mismatches(recs: np.ndarray, out: np.ndarray, limit: int = 8) -> list[str]:
                                not r["flags"] & _abi.F_UDP_S2)
                     if fut != (g["fut"] >= 0) or (fut and g["fut"] != int(r["sock"])):
                         err.append(f"future want {g['fut']}")
+                if g["tso"] == -1:
+                    err.append("tso probe ended before the layout test")
+                elif g["tso"] >= 0 and bool(int(r["flags"]) & _abi.F_TSO) != bool(g["tso"]):
+                    err.append(f"tso want {g['tso']}")
         if err:
             bad.append(f"[{i}] {', '.join(err)}: rec={r} ref={g}")
             if len(bad) >= limit:

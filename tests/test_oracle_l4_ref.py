@@ -84,7 +84,8 @@ def test_fixture_covers_the_rules():
     """The corpora reach every decision the fixture pins: all three TCP
     stages, both UDP stages with multi-match, the UDP future given up by a
     stage-2 match after a single stage-1 one, kernel hand-offs with and
-    without an L4 entry."""
+    without an L4 entry, the TCP timestamp-option layout test both ways
+    (every probe reached it)."""
     golden = np.load(GOLDEN)
     out = np.concatenate([l4_ref.load(golden, n)[0] for n in l4_ref.CORPORA])
     c = {k: out[:, i] for i, k in enumerate(l4_ref.COLS)}
@@ -96,6 +97,8 @@ def test_fixture_covers_the_rules():
     assert ((c["n1"] == 1) & udp & (c["fut"] >= 0)).any()
     assert ((c["kernel"] == 1) & (c["entry"] == 0)).any()
     assert ((c["kernel"] == 1) & tcp & (c["n1"] < 0)).any()   # TCP scattered
+    assert ((c["tso"] == 1) & tcp).any() and ((c["tso"] == 0) & tcp).any()
+    assert not (c["tso"] == -1).any() and not ((c["tso"] >= 0) & ~tcp).any()
 
 
 @pytest.mark.skipif(not os.path.exists(HARNESS), reason="oracle/_ref/ref_l4 is built only "
