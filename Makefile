@@ -11,7 +11,8 @@ CFLAGS   ?= -O2 -std=gnu11 -fPIC -Wall -Wextra -Wno-unused-parameter
 PRODUCT := onload_amd/liboo_gpu_rx.so
 PKTGEN  := onload_amd/liboo_pktgen.so
 SHIM    := onload_amd/liboo_rx_poll.so
-SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_rx_kernel_short.hip onload_amd/csrc/oo_table_kernel.hip \
+SRCS    := onload_amd/csrc/oo_rx_kernel.hip onload_amd/csrc/oo_rx_kernel_short.hip onload_amd/csrc/oo_rx_kernel_poll.hip \
+           onload_amd/csrc/oo_table_kernel.hip \
            onload_amd/csrc/oo_gpu_rx.cpp onload_amd/csrc/oo_gpu_rx_group.cpp onload_amd/csrc/oo_rx_csum.cpp
 HDRS    := include/oo_gpu_rx.h onload_amd/csrc/oo_rx_device.h
 
@@ -74,7 +75,7 @@ check-integration: oracle
 	  -I$(REF)/src/lib/transport/common -I$(REF)/src/lib/ciul -I$(REF)/src/lib/citools \
 	  -Iinclude -o build/netif_event_gpu.o integration/netif_event_gpu.c
 
-.PHONY: all oracle asm clean variants check-integration
+.PHONY: all oracle asm clean variants poll-variants check-integration
 
 tools/poll_rtt: tools/poll_rtt.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
@@ -91,3 +92,11 @@ tools/poll_bench: tools/poll_bench.c $(SHIM) $(PKTGEN) oracle include/oo_rx_poll
 	$(CC) $(CFLAGS) -Iinclude -o $@ tools/poll_bench.c -Lonload_amd -l:liboo_rx_poll.so \
 	  -l:liboo_gpu_rx.so -l:liboo_pktgen.so -Loracle -l:liboorx_oracle.so \
 	  -Wl,-rpath,'$$ORIGIN/../onload_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
+
+# Builds for tools/poll_ab.sh (build/pollvar/<name>/liboo_gpu_rx.so); not part
+# of `all`.
+POLL_VARIANTS ?= nodone:-DOO_POLL_DONE_MAX=0 nopoll:-DOO_POLL_MAX=0 inl0:-DOO_POLL_INLINE=0 \
+                  inl32:-DOO_POLL_INLINE=32
+poll-variants: $(SRCS) $(HDRS)
+	for v in $(POLL_VARIANTS); do n=$${v%%:*}; f=$$(echo "$${v#*:}" | tr ',' ' '); mkdir -p build/pollvar/$$n; \
+	  $(HIPCC) $(HIPFLAGS) $$f -shared -Wl,-soname,liboo_gpu_rx.so -o build/pollvar/$$n/liboo_gpu_rx.so $(SRCS) -ldl || exit 1; done

@@ -40,6 +40,8 @@ extern "C" int oo_rx_blocks_per_cu(void);
 extern "C" int oo_rx_launch_short(const oo_rx::KParams* P, int grid, hipStream_t stream);
 extern "C" int oo_rx_blocks_per_cu_short(void);
 extern "C" int oo_rx_waves_per_block(void);
+extern "C" int oo_rx_launch_poll(const oo_rx::PollArgs* A, int grid, hipStream_t stream);
+extern "C" int oo_rx_blocks_per_cu_poll(void);
 extern "C" int oo_rx_win_blocks_per_cu(void);
 extern "C" int oo_rx_body_blocks_per_cu(void);
 extern "C" int oo_rx_win_waves_per_block(void);
@@ -121,6 +123,15 @@ static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
 #endif
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
 constexpr uint32_t SMALL_N = 2048;    // launch(): batches up to this many packets take 8-packet tiles
+// The poll instance (auto) up to OO_POLL_MAX packets, writing a
+// submit_mapped batch's done word itself up to OO_POLL_DONE_MAX (build-time
+// knobs for same-box A/Bs: tools/poll_ab.sh).
+#ifndef OO_POLL_MAX
+#define OO_POLL_MAX 256
+#endif
+#ifndef OO_POLL_DONE_MAX
+#define OO_POLL_DONE_MAX 2048
+#endif
 constexpr int NTRACK = 8;             // streams tracked at once (LRU)
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
 // Tile-claim counter sets: two per tracked stream (its launches alternate
@@ -243,7 +254,15 @@ struct oo_gpu_rx_ctx {
   uint32_t gshift = ~0u;       // claim group of a wave: (gwave >> gshift) mod groups (~0u: per launch)
   uint32_t grid = 1024;        // resident blocks of rx_kernel
   uint32_t grid_short = 0;     // resident blocks of the short-frame rx_kernel (0: unused)
-  uint32_t ncu = 0, bpc[5] = {0, 0, 0, 0, 0};  // CUs; resident blocks per CU of the five kernels
+  uint32_t grid_poll = 0;      // resident blocks of the poll instance's rx_kernel (0: unused)
+  // A submit_mapped batch's completion, handed to launch(): the slot's done
+  // word and value, and the batch's descriptors in host memory (null: not
+  // known); launch() sets done_by_kernel when the poll instance writes it.
+  uint32_t* poll_done = nullptr;
+  uint32_t poll_done_val = 0;
+  const oo_gpu_pkt_desc* poll_h_desc = nullptr;
+  bool done_by_kernel = false;
+  uint32_t ncu = 0, bpc[6] = {0, 0, 0, 0, 0, 0};  // CUs; resident blocks per CU of the six kernels
   uint32_t grid_win = 0;       // resident blocks of win_kernel (split transform)
   uint32_t grid_body = 0;      // resident blocks of body_kernel
   uint32_t grid_body_gseq = 0; // ... of its per-group-sequence instance
@@ -815,6 +834,18 @@ bool in_reg(const oo_gpu_rx_ctx* c, const void* p, uint64_t bytes) {
   return false;
 }
 
+// The host address of [d, d + bytes) in a registered range, by its device
+// address (nullptr: not inside one).
+const void* host_of(const oo_gpu_rx_ctx* c, const void* d, uint64_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(d);
+  for (const HostReg& r : c->regs) {
+    const uintptr_t dlo = reinterpret_cast<uintptr_t>(r.dev), len = r.hi - r.lo;
+    if (a >= dlo && a - dlo <= len && bytes <= len - (a - dlo))
+      return reinterpret_cast<const void*>(r.lo + (a - dlo));
+  }
+  return nullptr;
+}
+
 int alloc_host_slots(oo_gpu_rx_ctx* c) {
   for (HostSlot& s : c->slot) {
     const uint64_t pk = c->stage_pkts;
@@ -851,6 +882,7 @@ void apply_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
   c->grid_win = grid(c->bpc[2]);
   c->grid_body = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]);
   c->grid_body_gseq = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[4]) : c->bpc[4]);
+  c->grid_poll = grid(c->bpc[5]);
   c->body_engine = t->body_engine;
   c->kx = t->walks == 0;
   c->kmode = t->path;
@@ -870,7 +902,7 @@ extern "C" {
 int oo_gpu_rx_abi_version(void) { return OO_GPU_RX_ABI_VERSION; }
 
 int oo_gpu_rx_set_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
-  if (c == nullptr || (t != nullptr && (t->path > 3 || t->grid_pct > 100 || t->body_engine > 2 ||
+  if (c == nullptr || (t != nullptr && (t->path > 4 || t->grid_pct > 100 || t->body_engine > 2 ||
                                   t->walks > 1))) return -EINVAL;
   apply_tuning(c, t);
   return 0;
@@ -919,9 +951,10 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) {
     // Persistent grids: every resident block (occupancy query).
     c->ncu = (uint32_t)prop.multiProcessorCount;
-    const int b[5] = {oo_rx_blocks_per_cu(), oo_rx_blocks_per_cu_short(), oo_rx_win_blocks_per_cu(),
-                      oo_rx_body_blocks_per_cu(), oo_rx_body_blocks_per_cu_gseq()};
-    for (int k = 0; k < 5; ++k) c->bpc[k] = (uint32_t)std::max(0, b[k]);
+    const int b[6] = {oo_rx_blocks_per_cu(), oo_rx_blocks_per_cu_short(), oo_rx_win_blocks_per_cu(),
+                      oo_rx_body_blocks_per_cu(), oo_rx_body_blocks_per_cu_gseq(),
+                      oo_rx_blocks_per_cu_poll()};
+    for (int k = 0; k < 6; ++k) c->bpc[k] = (uint32_t)std::max(0, b[k]);
   }
   apply_tuning(c, nullptr);
   DevTables& T = c->T;
@@ -1413,17 +1446,27 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
     sample_lengths(c, P, n, s);
     return 0;
   }
-  const bool use_short = !tx && c->grid_short > 0 && (c->kmode == 2 || (c->kmode == 0 && short_frames));
+  const bool small = n <= SMALL_N;
+  // A poll's batch (at most OO_POLL_MAX packets) takes the poll instance (a
+  // 12-slot ring: a tile's frames requested whole with its windows;
+  // descriptors in the kernel arguments; its own completion word --
+  // oo_rx_kernel.hip "The poll instance").  Same-box A/B, config 2 zero
+  // copy: 16 / 64 events -4.5 / -3.9 us per poll, 256 level, 1024 +5 us
+  // (profiles/r05/poll_ab_*.jsonl).
+  const bool use_poll =
+      !tx && c->grid_poll > 0 && (c->kmode == 4 || (c->kmode == 0 && small && n <= OO_POLL_MAX));
+  const bool use_short =
+      !use_poll && !tx && c->grid_short > 0 && (c->kmode == 2 || (c->kmode == 0 && short_frames));
   const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
   // A small batch (a poll's worth: at most SMALL_N packets) is cut into tiles
   // of 8 packets, a wave each, statically: its bodies stream in parallel, so
   // the batch takes about one tile's latency -- over PCIe (frames read in
   // place from host memory) one 64-packet tile's 12 KiB in flight would take
   // many round trips.  Larger batches: full 64-packet tiles.
-  const bool small = n <= SMALL_N;
   const uint32_t need = small ? (n + 7) / 8 : (n + 63) / 64;  // waves, a tile each
   const uint32_t blocks = std::max<uint32_t>(
-      1, std::min<uint32_t>((need + wpb - 1) / wpb, use_short ? c->grid_short : c->grid));
+      1, std::min<uint32_t>((need + wpb - 1) / wpb,
+                            use_poll ? c->grid_poll : use_short ? c->grid_short : c->grid));
   const uint64_t W = (uint64_t)blocks * wpb;
   // The launch's claim counters (zeroed by the stream's previous launch),
   // one per wave group.  Short frames (under 1 KiB of buffer per packet:
@@ -1452,13 +1495,29 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
     P.tstep = (uint32_t)step;
   }
   const int grid = (int)blocks;
-  const int rc = tx ? oo_tx_launch(&P, grid, s)
-                    : use_short ? oo_rx_launch_short(&P, grid, s) : oo_rx_launch(&P, grid, s);
+  int rc;
+  if (use_poll) {
+    oo_rx::PollArgs A;
+    A.P = P;
+    A.done_ctr = P.claim + 32u * oo_rx::FLAG_LINE;
+    A.done = n <= OO_POLL_DONE_MAX ? c->poll_done : nullptr;
+    A.done_val = c->poll_done_val;
+    A.rsvd = 0;
+    if (c->poll_h_desc != nullptr && n <= oo_rx::POLL_INLINE && P.ring_mask == ~0u) {
+      memcpy(A.d, c->poll_h_desc, sizeof(oo_gpu_pkt_desc) * n);
+      A.P.desc = nullptr;  // read from the kernel arguments
+    }
+    rc = oo_rx_launch_poll(&A, grid, s);
+    if (rc == 0 && A.done != nullptr) c->done_by_kernel = true;
+  } else {
+    rc = tx ? oo_tx_launch(&P, grid, s)
+            : use_short ? oo_rx_launch_short(&P, grid, s) : oo_rx_launch(&P, grid, s);
+  }
   if (rc != 0) return -EIO;  // (nothing ran: the set stays zero for the next launch)
   trk->parity ^= 1u;
   if (!tx) {
     note_launch(trk);
-    c->last_path = use_short ? 2u : 1u;
+    c->last_path = use_poll ? 5u : use_short ? 2u : 1u;
     sample_lengths(c, P, n, s);
   }
   return 0;
@@ -1685,12 +1744,23 @@ int oo_gpu_rx_submit_mapped(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t fra
     if (rc < 0) return rc;
   }
   hipStream_t st = s.stream;
+  bool by_kernel = false;  // the poll instance writes the done word itself
   if (n > 0) {
     int rc = prepare(c, st);
-    if (rc == 0) rc = launch(c, d_frames, frames_bytes, d_desc, n, d_out, nullptr, st);
+    if (rc == 0) {
+      c->poll_done = s.d_done;
+      c->poll_done_val = done_word(t);
+      c->poll_h_desc = static_cast<const oo_gpu_pkt_desc*>(host_of(c, d_desc, sizeof(oo_gpu_pkt_desc) * n));
+      c->done_by_kernel = false;
+      rc = launch(c, d_frames, frames_bytes, d_desc, n, d_out, nullptr, st);
+      by_kernel = rc == 0 && c->done_by_kernel;
+      c->poll_done = nullptr;
+      c->poll_h_desc = nullptr;
+      c->done_by_kernel = false;
+    }
     if (rc) return rc;
   }
-  if (hipStreamWriteValue32(st, s.d_done, done_word(t), 0) != hipSuccess ||
+  if ((!by_kernel && hipStreamWriteValue32(st, s.d_done, done_word(t), 0) != hipSuccess) ||
       hipEventRecord(s.done, st) != hipSuccess)
     return -EIO;
   s.busy = true;

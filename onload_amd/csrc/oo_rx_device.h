@@ -5,6 +5,7 @@
 #ifndef OO_RX_DEVICE_H
 #define OO_RX_DEVICE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/oo_gpu_rx.h"
@@ -260,6 +261,25 @@ struct KParams {
   const uint32_t* kx_ok;
   uint32_t kx_nb4, kx_ne6;
 };
+
+// The poll instance's kernel arguments (oo_rx_kernel.hip "The poll
+// instance"): the batch's KParams, its completion (done null: none) and, for
+// a batch of at most POLL_INLINE packets launched with P.desc null, its
+// descriptors.  2.3 KiB, within the 4-KiB kernel-argument limit.
+#ifndef OO_POLL_INLINE
+#define OO_POLL_INLINE 128
+#endif
+constexpr uint32_t POLL_INLINE = OO_POLL_INLINE;
+struct PollArgs {
+  KParams P;
+  uint32_t* done_ctr;  // the launch's claim-set FLAG_LINE word (0 at launch)
+  uint32_t* done;      // host-mapped word: done_val once every record has landed
+  uint32_t done_val;
+  uint32_t rsvd;
+  oo_gpu_pkt_desc d[POLL_INLINE > 0 ? POLL_INLINE : 1];
+};
+constexpr uint64_t POLL_DESC_OFF = offsetof(PollArgs, d);
+static_assert(POLL_DESC_OFF % 16 == 0 && sizeof(PollArgs) <= 4096, "PollArgs layout");
 
 }  // namespace oo_rx
 

@@ -54,7 +54,12 @@
 // OO_RX_SHORT (oo_rx_kernel_short.hip): the same rx_kernel with a 2-slot
 // ring, compiled into namespace oo_rx_short for short-frame batches (no
 // tx_kernel there: its check-field staging needs a 4-slot ring).
-#ifdef OO_RX_SHORT
+// OO_RX_POLL (oo_rx_kernel_poll.hip): rx_kernel alone, for a poll's batch,
+// in namespace oo_rx_poll (see "The poll instance" at its kernel).
+#if defined(OO_RX_POLL)
+namespace oo_rx_poll {
+using namespace ::oo_rx;
+#elif defined(OO_RX_SHORT)
 namespace oo_rx_short {
 using namespace ::oo_rx;
 #else
@@ -2030,8 +2035,22 @@ __device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, 
 
 // Where lane `lane` of unit t loads its descriptor from (lanes without a
 // packet: some other in-bounds entry).
+#ifdef OO_RX_POLL
+// The poll instance: a batch of at most POLL_INLINE packets may bring its
+// descriptors in the kernel arguments (P.desc null: PollArgs::d), read from
+// where the launch put them instead of over PCIe from the caller's memory.
+__device__ __forceinline__ uint64_t desc_base(const KParams& P) {
+  return P.desc != nullptr
+             ? reinterpret_cast<uint64_t>(P.desc)
+             : reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + POLL_DESC_OFF;
+}
+#else
+__device__ __forceinline__ uint64_t desc_base(const KParams& P) {
+  return reinterpret_cast<uint64_t>(P.desc);
+}
+#endif
 __device__ __forceinline__ uint64_t desc_at(const KParams& P, uint32_t i) {
-  return reinterpret_cast<uint64_t>(P.desc) + (uint64_t)((P.ring_cons + i) & P.ring_mask) * 16;
+  return desc_base(P) + (uint64_t)((P.ring_cons + i) & P.ring_mask) * 16;
 }
 __device__ __forceinline__ uint64_t desc_src(const KParams& P, const Unit& t, uint32_t lane) {
   return desc_at(P, lane < t.cnt ? t.first + lane : lane % P.n);
@@ -2700,9 +2719,42 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
   }  // gwave < P.ntiles
 }
 
+#ifdef OO_RX_POLL
+// ---------------------------------------------------------------------------
+// The poll instance (oo_rx_kernel_poll.hip): a poll's batch
+// of at most a few thousand packets, its frames often read in place over
+// PCIe, is bound by its chain of round trips, not by bytes.  The same tile
+// loop, with a ring deep enough (OO_RX_RING 12) that a tile of eight
+// 1514-B frames issues its whole body with its header windows -- one round
+// trip for the frames, where the 4-slot ring waits three -- its descriptors
+// from the kernel arguments when they fit there (desc_base), and its own
+// completion: each wave, once its record stores have completed, counts
+// itself in the launch's claim-set FLAG_LINE word (zeroed by the stream's
+// previous launch), and the last one writes the caller's done word in host
+// memory -- no second operation on the stream after the kernel.
+__device__ __forceinline__ void poll_done(const PollArgs& A) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (lane == 0) {
+    const uint32_t prev =
+        __hip_atomic_fetch_add(A.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (prev + 1u == gridDim.x * (uint32_t)WAVES)
+      __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// (Few waves per launch: no occupancy target; the deep ring's unrolled
+// rounds take more registers than three waves per SIMD allow.)
+__global__ __launch_bounds__(WAVES * 64) void rx_kernel(PollArgs A) {
+  tile_loop<false>(A.P);
+  if (A.done != nullptr) poll_done(A);
+}
+#else
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void rx_kernel(KParams P) {
   tile_loop<false>(P);
 }
+#endif
+#ifndef OO_RX_POLL
 #ifndef OO_RX_SHORT
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void tx_kernel(KParams P) {
   tile_loop<true>(P);
@@ -3240,10 +3292,24 @@ __device__ __forceinline__ void body_loop(const KParams& P) {
 #endif  // OO_RX_GSEQ
 
 __global__ __launch_bounds__(WAVES_B * 64) void body_kernel(KParams P) { body_loop(P); }
+#endif  // !OO_RX_POLL
 
 }  // namespace oo_rx
 
-#ifdef OO_RX_SHORT
+#if defined(OO_RX_POLL)
+extern "C" int oo_rx_blocks_per_cu_poll(void) {
+  int b = 0;
+  const hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, oo_rx_poll::rx_kernel, oo_rx_poll::WAVES * 64, 0);
+  return e == hipSuccess ? b : 0;
+}
+
+// Launch one poll-sized RX batch on `stream` (oo_rx_poll::rx_kernel).
+extern "C" int oo_rx_launch_poll(const oo_rx::PollArgs* A, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx_poll::rx_kernel, dim3(grid), dim3(oo_rx_poll::WAVES * 64), 0, stream, *A);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#elif defined(OO_RX_SHORT)
 // Resident blocks per CU of the short-frame rx_kernel.
 extern "C" int oo_rx_blocks_per_cu_short(void) {
   int b = 0;

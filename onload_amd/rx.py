@@ -206,7 +206,7 @@ class GpuRxStack:
     def last_path(self) -> int:
         """oo_gpu_rx_last_path: the last batch's kernels (1 / 2 rx_kernel
         instances, 3 / 4 the split transform with the lockstep / sequences
-        body engine, 0 none yet)."""
+        body engine, 5 the poll instance, 0 none yet)."""
         return int(self._lib.oo_gpu_rx_last_path(self._ctx))
 
     def set_len_hint(self, mean_frame_len: int) -> None:

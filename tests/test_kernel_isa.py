@@ -24,6 +24,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "onload_amd", "csrc", "oo_rx_kernel.hip")
 SRC_SHORT = os.path.join(ROOT, "onload_amd", "csrc", "oo_rx_kernel_short.hip")
 RX_SHORT = "_ZN11oo_rx_short9rx_kernelEN5oo_rx7KParamsE"
+SRC_POLL = os.path.join(ROOT, "onload_amd", "csrc", "oo_rx_kernel_poll.hip")
+RX_POLL = "_ZN10oo_rx_poll9rx_kernelEN5oo_rx8PollArgsE"
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
@@ -104,6 +106,33 @@ def test_short_kernel_same_invariants(asm_short):
     assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
     assert len(re.findall(r"global_store_dword\b", rx)) == 3  # zero_claim_set
     assert not re.findall(r"flat_store|flat_load|flat_atomic", rx)
+
+
+@pytest.fixture(scope="module")
+def asm_poll(tmp_path_factory):
+    """The poll instance (12-slot ring, oo_rx_kernel_poll.hip)."""
+    return _compile(tmp_path_factory, SRC_POLL)
+
+
+def test_poll_kernel_same_invariants(asm_poll):
+    """The poll instance: no scratch and the same stores per tile; besides
+    zero_claim_set's three, one more 4-B `sc0 sc1` store -- the done word,
+    after the wave's last wait -- and the one returning system-scope add
+    that counts the wave out (oo_rx_kernel.hip "The poll instance")."""
+    text, stderr = asm_poll
+    u = _usage(stderr, RX_POLL)
+    assert u["VGPRs Spill"] == 0, u
+    assert u["VGPRs"] <= 256, u
+    rx = _body(text, RX_POLL)
+    assert "scratch_" not in rx
+    assert len(re.findall(r"global_store_dwordx4", rx)) == 2
+    assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
+    assert len(re.findall(r"global_store_dword\b", rx)) == 4
+    assert len(re.findall(r"global_store_dword .* sc0 sc1$", rx, re.M)) == 1
+    assert len(re.findall(r"global_atomic_add .* sc0 sc1$", rx, re.M)) == 1
+    assert not re.findall(r"flat_store|flat_load|flat_atomic", rx)
+    # the kernel holds rx_kernel alone
+    assert "tx_kernel" not in text and "win_kernel" not in text
 
 
 WIN = "_ZN5oo_rx10win_kernelENS_7KParamsE"

@@ -20,13 +20,13 @@ def _tuning(**kw):
 def test_tuning_validated():
     g = GpuRxStack(device=-1, max_socks=16, ip6_log2=4)
     g.set_tuning(None)
-    for path in (0, 1, 2, 3):
+    for path in (0, 1, 2, 3, 4):
         g.set_tuning(_tuning(path=path))
     for engine in (0, 1, 2):
         g.set_tuning(_tuning(path=3, body_engine=engine))
     for walks in (0, 1):
         g.set_tuning(_tuning(walks=walks))
-    for bad in (dict(path=4), dict(grid_pct=101), dict(body_engine=3), dict(walks=2)):
+    for bad in (dict(path=5), dict(grid_pct=101), dict(body_engine=3), dict(walks=2)):
         with pytest.raises(OSError):
             g.set_tuning(_tuning(**bad))
     g.close()
