@@ -19,7 +19,8 @@
  * OO_RX_POLL_CROSSOVER: a chunk the cost model prices below the device
  * batch goes back through other_ev, and this program's other_ev runs the
  * per-event CPU loop on it inside the timed poll -- the deployed shape).
- * The last line fits the model's constants to the runs.
+ * The crossover model's defaults (src/shim/oo_rx_poll.c gpu_pays) are fitted
+ * to these lines.
  */
 #include <errno.h>
 #include <stdio.h>
