@@ -256,8 +256,9 @@ def test_poll_crossover(cuda, zero_copy):
     assert [r.tobytes() if hasattr(r, "tobytes") else r for r in rec.recs] == \
         [r.tobytes() if hasattr(r, "tobytes") else r for r in base_rec.recs]
     assert st == base_st
-    # per chunk: fixed = 40 frames' worth of the CPU's per-frame saving
-    per = {"cpu_pkt_ps": 20000, "cpu_byte_ps": 0, "gpu_pkt_ps": 10000, "gpu_byte_ps": 0,
+    # per chunk: fixed = 40 frames' worth of the CPU's per-frame saving (the
+    # per-byte terms 1 ps each: 0 would take the defaults)
+    per = {"cpu_pkt_ps": 20000, "cpu_byte_ps": 1, "gpu_pkt_ps": 10000, "gpu_byte_ps": 1,
            "gpu_fixed_ns": 400}
     rec, st = run(per)
     cut = (n // 64) * 64
@@ -301,8 +302,9 @@ def test_poll_table_change_then_rest_handed_back(cuda):
                 removed.append(g.filter_remove(*filters[0]))
             super().full_handler(i, r)
 
-    # per chunk: fixed = 40 frames' worth of the CPU's per-frame saving
-    per = {"cpu_pkt_ps": 20000, "cpu_byte_ps": 0, "gpu_pkt_ps": 10000, "gpu_byte_ps": 0,
+    # per chunk: fixed = 40 frames' worth of the CPU's per-frame saving (the
+    # per-byte terms 1 ps each: 0 would take the defaults)
+    per = {"cpu_pkt_ps": 20000, "cpu_byte_ps": 1, "gpu_pkt_ps": 10000, "gpu_byte_ps": 1,
            "gpu_fixed_ns": 400}
     rec = Closer()
     p = poll.RxPoll(g, pool, 2048, epp, True, rec, crossover=per)
