@@ -110,7 +110,8 @@ for l in open("'"$OUT"'/poll_ab.jsonl"):
     d = json.loads(l)
     if d["mode"] == "zero_copy": print(d["variant"], d["config"], d["evs_per_poll"], d["poll_us_median"], d["cpu_poll_us_equiv"])' ;;
     stamps)
-      timeout -k 10 300 python tools/stamps.py ${STAMP_CONFIG:-3} > "$OUT/stamps.txt" 2> "$OUT/stamps.err" \
+      OO_RX_LIB="${OO_RX_LIB:-build/var_st.so}" timeout -k 10 300 python tools/stamps.py --config ${STAMP_CONFIG:-3} \
+        > "$OUT/stamps.txt" 2> "$OUT/stamps.err" \
         || fail stamps $? "$OUT/stamps.err"
       tail -c 600 "$OUT/stamps.txt"; echo ;;
     *) echo "unknown step $step"; exit 2 ;;
