@@ -236,7 +236,8 @@ uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* ctx);
  * 4-slot ring, 2 its 2-slot instance, 3 the split transform (win_kernel +
  * body_kernel with lockstep slots), 4 the split transform with the
  * per-group-sequence body_kernel, 5 the poll instance (12-slot ring, for
- * batches of at most 256 packets); 0 none yet.  For measurements: which
+ * batches of at most 256 packets), 6 the resident poll kernel (the same
+ * tile loop, no launch: oo_gpu_rx_get_resident_stats); 0 none yet.  For measurements: which
  * kernels a timed launch's duration covers. */
 uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* ctx);
 /* Table maintenance so far: flushes of queued changes to the device, and how
@@ -252,6 +253,22 @@ typedef struct oo_gpu_rx_table_stats {
   uint32_t rsvd;
 } oo_gpu_rx_table_stats;
 int oo_gpu_rx_get_table_stats(oo_gpu_rx_ctx* ctx, oo_gpu_rx_table_stats* out);
+/* The resident poll kernel: a context that submits
+ * oo_gpu_rx_submit_mapped batches of at most 256 packets starts a small
+ * grid that stays on the device and takes them from a doorbell in host
+ * memory, with no launch per batch; it leaves after 200 ms without one (and
+ * when the context closes).  Until it runs, and whenever it may have left,
+ * batches take the launch path.  Counts so far: batches it took, of them
+ * re-run through a launch (it had left before taking them), instances
+ * started; running: one was seen polling and was rung within its window.
+ * For tests and measurements. */
+typedef struct oo_gpu_rx_resident_stats {
+  uint64_t batches;
+  uint64_t fallbacks;
+  uint32_t instances;
+  uint32_t running;
+} oo_gpu_rx_resident_stats;
+int oo_gpu_rx_get_resident_stats(const oo_gpu_rx_ctx* ctx, oo_gpu_rx_resident_stats* out);
 /* Streams.  The context remembers the streams it launched on (nothing is
  * recorded per batch): a table change enqueues an event on each of them at
  * that moment and waits for it, so every stream used with the context must

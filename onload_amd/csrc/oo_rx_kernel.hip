@@ -2437,7 +2437,11 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
   const uint32_t hi = lane & 1u;
   const uint32_t last = t.cnt - 1u;
-  uint4* const out = reinterpret_cast<uint4*>(P.out);
+  // (a global pointer whatever P.out came from: the resident kernel reads
+  // it from host memory, where a generic pointer would make these flat
+  // stores, counted in lgkmcnt as well)
+  __attribute__((address_space(1))) u32x4* const out =
+      (__attribute__((address_space(1))) u32x4*)reinterpret_cast<uintptr_t>(P.out);
 #pragma unroll
   for (uint32_t u = 0; u < 2; ++u) {
     const uint32_t q = min(32u * u + (lane >> 1), last);
@@ -2448,7 +2452,7 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
       const uint32_t a = lane_get(w[d], q), b = lane_get(w[4 + d], q);
       vw[d] = hi ? b : a;
     }
-    out[(size_t)(t.first + q) * 2u + hi] = v;
+    out[(size_t)(t.first + q) * 2u + hi] = u32x4{v.x, v.y, v.z, v.w};
   }
 }
 
@@ -2748,6 +2752,88 @@ __device__ __forceinline__ void poll_done(const PollArgs& A) {
 __global__ __launch_bounds__(WAVES * 64) void rx_kernel(PollArgs A) {
   tile_loop<false>(A.P);
   if (A.done != nullptr) poll_done(A);
+}
+
+// ---------------------------------------------------------------------------
+// The resident poll kernel: the poll instance's tile
+// loop run for batch after batch by a small grid that stays on the device,
+// so a poll's batch pays no launch.  The host writes batch k's mailbox
+// (ResMail: frames, descriptors, records, partition, the slot's done word)
+// and then the doorbell = k.  In each block one lane polls the doorbell in
+// host memory (sleeping between reads) and the block's waves run every batch
+// up to the value read, in order; per batch each wave counts itself out as
+// poll_done does (counter by batch parity; the last resets the other
+// parity's counter before it writes the done word).  A mailbox flagged with
+// a table change (RES_TABLES in its tstep word) makes each wave drop its
+// cached table lines first (agent-scope acquire).  Every block leaves once the doorbell reads
+// RES_QUIT or after idle_ticks without a new batch: the host rings only
+// while well inside that window (oo_gpu_rx.cpp res_usable), so no block
+// leaves with a batch outstanding.
+__device__ __forceinline__ uint64_t mail_word2(const uint32_t (&w)[16], int k) {
+  return (uint64_t)w[k] | ((uint64_t)w[k + 1] << 32);
+}
+
+__global__ __launch_bounds__(WAVES * 64) void rx_resident(ResArgs A) {
+  __shared__ uint32_t s_bell;
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(A.alive, A.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t seen = A.seq0;
+  uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t v;
+      for (;;) {
+        v = __hip_atomic_load(A.doorbell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v != seen) break;
+        if (__builtin_amdgcn_s_memrealtime() - t_idle > A.idle_ticks) {
+          v = RES_QUIT;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_bell = v;
+    }
+    __syncthreads();
+    const uint32_t bell = s_bell;
+    __syncthreads();  // (s_bell is rewritten only after every wave read it)
+    if (bell == RES_QUIT) break;
+    while (seen != bell) {
+      ++seen;
+      // The batch's mailbox: lanes 0..15 read its sixteen words (system
+      // scope: from host memory, after the doorbell).
+      const uint32_t* const mw = reinterpret_cast<const uint32_t*>(A.mail + seen % RES_SLOTS);
+      const uint32_t mv =
+          __hip_atomic_load(mw + (lane & 15u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = (uint32_t)__builtin_amdgcn_readlane((int)mv, k);
+      if (w[14] & RES_TABLES) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      KParams P = A.P;
+      P.frames = reinterpret_cast<const uint8_t*>(mail_word2(w, 0));
+      P.frames_bytes = mail_word2(w, 2);
+      P.desc = reinterpret_cast<const oo_gpu_pkt_desc*>(mail_word2(w, 4));
+      P.out = reinterpret_cast<oo_gpu_rx_result*>(mail_word2(w, 6));
+      P.n = w[10];
+      P.ntiles = w[11];
+      P.tlo = w[12];
+      P.ta = w[13];
+      P.tstep = w[14] & 0xffu;
+      tile_loop<false>(P);
+      // Counted out (poll_done, by batch parity).
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        uint32_t* const ctr = A.ctr + 32u * (seen & 1u);
+        const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (prev + 1u == gridDim.x * (uint32_t)WAVES) {
+          __hip_atomic_store(A.ctr + 32u * ((seen + 1u) & 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)mail_word2(w, 8), w[15],
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+    t_idle = __builtin_amdgcn_s_memrealtime();
+  }
 }
 #else
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void rx_kernel(KParams P) {
@@ -3307,6 +3393,13 @@ extern "C" int oo_rx_blocks_per_cu_poll(void) {
 // Launch one poll-sized RX batch on `stream` (oo_rx_poll::rx_kernel).
 extern "C" int oo_rx_launch_poll(const oo_rx::PollArgs* A, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(oo_rx_poll::rx_kernel, dim3(grid), dim3(oo_rx_poll::WAVES * 64), 0, stream, *A);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Start the resident poll kernel on `stream` (it stays until the doorbell
+// reads RES_QUIT or it has idled for A->idle_ticks).
+extern "C" int oo_rx_launch_resident(const oo_rx::ResArgs* A, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(oo_rx_poll::rx_resident, dim3(grid), dim3(oo_rx_poll::WAVES * 64), 0, stream, *A);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #elif defined(OO_RX_SHORT)
