@@ -298,6 +298,7 @@ struct oo_gpu_rx_ctx {
   int64_t res_last_ns = 0;
   uint64_t res_tables_gen = ~0ull;
   uint64_t n_res = 0, n_res_fallback = 0;
+  std::vector<void*> retired;  // replaced pending-word buffers (freed at close)
   uint32_t ncu = 0, bpc[6] = {0, 0, 0, 0, 0, 0};  // CUs; resident blocks per CU of the six kernels
   uint32_t grid_win = 0;       // resident blocks of win_kernel (split transform)
   uint32_t grid_body = 0;      // resident blocks of body_kernel
@@ -674,6 +675,7 @@ void free_dev(oo_gpu_rx_ctx* c) {
     if (t.ev) (void)hipEventDestroy(t.ev);
     if (t.pend) (void)hipFree(t.pend);
   }
+  for (void* p : c->retired) (void)hipFree(p);
   for (const HostReg& r : c->regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.lo));
   if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
   if (c->res_s) (void)hipStreamDestroy(c->res_s);
@@ -1373,8 +1375,12 @@ static void sample_lengths(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n, hipSt
 }
 
 // The split transform (oo_rx_kernel.hip "The split transform"): win_kernel,
-// then body_kernel, on s.  The stream's pending-word buffer grows in stream
-// order (hipMallocAsync), so no call waits for the device.
+// then body_kernel, on s.  The stream's pending-word buffer grows by a new
+// allocation (hipMalloc: no wait for the device); the one it replaces may
+// still be read by launches in flight, so it is kept until the context
+// closes (growth is monotonic: a few buffers at most).  No stream-ordered
+// allocator: its memory freed with hipFree at close was a mix the runtime
+// does not promise to support.
 static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Tracked* trk,
                         uint32_t* set, hipStream_t s, bool seq_body) {
   // Mixed sizes (the short-frame class's IMIX, or a sampled profile): the
@@ -1382,11 +1388,18 @@ static int launch_split(oo_gpu_rx_ctx* c, const KParams& base, uint32_t n, Track
   const bool gseq = c->body_engine ? c->body_engine == 2 : seq_body;
   const uint32_t grid_body = gseq ? c->grid_body_gseq : c->grid_body;
   if (trk->pend_n < (uint64_t)n + 64) {
-    if (trk->pend != nullptr && hipFreeAsync(trk->pend, s) != hipSuccess) return -EIO;
-    trk->pend = nullptr;
-    trk->pend_n = 0;
     const uint64_t want = std::max<uint64_t>((uint64_t)n + 64, 1u << 16);
-    if (hipMallocAsync(reinterpret_cast<void**>(&trk->pend), want * 8, s) != hipSuccess) return -ENOMEM;
+    uint64_t* fresh = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&fresh), want * 8) != hipSuccess) return -ENOMEM;
+    if (trk->pend != nullptr) {
+      try {
+        c->retired.push_back(trk->pend);
+      } catch (...) {
+        (void)hipFree(fresh);
+        return -ENOMEM;
+      }
+    }
+    trk->pend = fresh;
     trk->pend_n = want;
   }
   KParams B = base, A = base;
