@@ -265,9 +265,12 @@ struct KParams {
 // The poll instance's kernel arguments (oo_rx_kernel.hip "The poll
 // instance"): the batch's KParams, its completion (done null: none) and, for
 // a batch of at most POLL_INLINE packets launched with P.desc null, its
-// descriptors.  2.3 KiB, within the 4-KiB kernel-argument limit.
+// descriptors.  Off by default (OO_POLL_INLINE 0: 16 B of them): with 128
+// descriptors the arguments are 2.3 KiB a launch, and the GPU faults of this
+// round came only with such launches in the process;
+// the saving was ~1 us a poll.
 #ifndef OO_POLL_INLINE
-#define OO_POLL_INLINE 128
+#define OO_POLL_INLINE 0
 #endif
 constexpr uint32_t POLL_INLINE = OO_POLL_INLINE;
 struct PollArgs {
