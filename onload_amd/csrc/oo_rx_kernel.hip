@@ -2761,9 +2761,9 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(PollArgs A) {
 // (ResMail: frames, descriptors, records, partition, the slot's done word)
 // and then the doorbell = k.  In each block one lane polls the doorbell in
 // host memory (sleeping between reads) and the block's waves run every batch
-// up to the value read, in order; per batch each wave counts itself out as
-// poll_done does (counter by batch parity; the last resets the other
-// parity's counter before it writes the done word).  A mailbox flagged with
+// up to the value read, in order; per batch each wave with a tile counts
+// itself out as poll_done does (counter by batch parity; the last resets the
+// other parity's counter before it writes the done word).  A mailbox flagged with
 // a table change (RES_TABLES in its tstep word) makes each wave drop its
 // cached table lines first (agent-scope acquire).  Every block leaves once the doorbell reads
 // RES_QUIT or after idle_ticks without a new batch: the host rings only
@@ -2820,12 +2820,15 @@ __global__ __launch_bounds__(WAVES * 64) void rx_resident(ResArgs A) {
       P.ta = w[13];
       P.tstep = w[14] & 0xffu;
       tile_loop<false>(P);
-      // Counted out (poll_done, by batch parity).
+      // Counted out (poll_done, by batch parity): the waves that had a tile
+      // (waves 0 .. ntiles-1; ntiles <= the grid's waves), so the done word
+      // does not wait for blocks that saw the doorbell late and had nothing.
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
+      const uint32_t gw = blockIdx.x * (uint32_t)WAVES + (threadIdx.x >> 6);
+      if (lane == 0 && gw < P.ntiles) {
         uint32_t* const ctr = A.ctr + 32u * (seen & 1u);
         const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (prev + 1u == gridDim.x * (uint32_t)WAVES) {
+        if (prev + 1u == P.ntiles) {
           __hip_atomic_store(A.ctr + 32u * ((seen + 1u) & 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)mail_word2(w, 8), w[15],
                              __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
