@@ -235,9 +235,10 @@ uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* ctx);
 /* Which kernels transformed the context's last batch: 1 rx_kernel with the
  * 4-slot ring, 2 its 2-slot instance, 3 the split transform (win_kernel +
  * body_kernel with lockstep slots), 4 the split transform with the
- * per-group-sequence body_kernel, 5 the poll instance (12-slot ring, for
- * batches of at most 256 packets), 6 the resident poll kernel (the same
- * tile loop, no launch: oo_gpu_rx_get_resident_stats); 0 none yet.  For measurements: which
+ * per-group-sequence body_kernel, 5 the poll instance (12-slot ring: path
+ * 4, or in a library built with OO_POLL_MAX=256 batches of at most 256
+ * packets), 6 the resident poll kernel (the same tile loop, no launch; in a
+ * library built with OO_RES_MAX=256); 0 none yet.  For measurements: which
  * kernels a timed launch's duration covers. */
 uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* ctx);
 /* Table maintenance so far: flushes of queued changes to the device, and how
@@ -253,7 +254,8 @@ typedef struct oo_gpu_rx_table_stats {
   uint32_t rsvd;
 } oo_gpu_rx_table_stats;
 int oo_gpu_rx_get_table_stats(oo_gpu_rx_ctx* ctx, oo_gpu_rx_table_stats* out);
-/* The resident poll kernel: a context that submits
+/* The resident poll kernel (built in with OO_RES_MAX=256,
+ * off by default): a context that submits
  * oo_gpu_rx_submit_mapped batches of at most 256 packets starts a small
  * grid that stays on the device and takes them from a doorbell in host
  * memory, with no launch per batch; it leaves after 200 ms without one (and
@@ -312,7 +314,7 @@ int oo_gpu_rx_set_len_hint(oo_gpu_rx_ctx* ctx, uint32_t mean_frame_len);
  * measured fastest.  The library reads no environment: a deployment gets
  * exactly these defaults unless it calls this.  0 or -EINVAL. */
 typedef struct oo_gpu_rx_tuning {
-  uint32_t path;           /* 0 auto (at most 256 packets: 4; frames within
+  uint32_t path;           /* 0 auto (frames within
                               the 128-B header window, 2^20+ packets: 3;
                               mixed sizes with long frames, 2^16+: 3; else 2
                               for under 1 KiB of buffer per packet, 1
@@ -321,8 +323,7 @@ typedef struct oo_gpu_rx_tuning {
                               2 the same with the 2-slot ring; 3 the split
                               transform (win_kernel + body_kernel); 4 the
                               poll instance (12-slot ring; a submit_mapped
-                              batch's descriptors in the kernel arguments
-                              and its completion written by the kernel)     */
+                              batch's completion written by the kernel)    */
   uint32_t grid_pct;       /* % of the resident grid to launch (0: 100)       */
   uint32_t groups;         /* tile-claim groups at most (0: by frame size)    */
   int32_t  gshift;         /* a group's wave runs, log2 (-1: by frame size)   */

@@ -126,12 +126,17 @@ constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 K
 constexpr uint32_t SMALL_N = 2048;    // launch(): batches up to this many packets take 8-packet tiles
 // The poll instance (auto) up to OO_POLL_MAX packets, writing a
 // submit_mapped batch's done word itself up to OO_POLL_DONE_MAX (build-time
-// knobs for same-box A/Bs: tools/poll_ab.sh).
+// knobs for same-box A/Bs: tools/poll_ab.sh).  Off by default (0; the tuning
+// path 4 still forces it): every process in which the GPU faulted this round
+// had run it, none before it went in; the cause is
+// not found.  Built with OO_POLL_MAX=256 OO_RES_MAX=256 (make poll-variants:
+// pollres) it takes a poll's batches, and the resident kernel those of
+// oo_gpu_rx_submit_mapped.
 // The resident poll kernel (oo_rx_kernel.hip "The resident poll kernel")
 // takes submit_mapped batches of at most OO_RES_MAX packets (0: never) once
 // it runs; OO_RES_WAVES waves, a tile of eight packets each.
 #ifndef OO_RES_MAX
-#define OO_RES_MAX 256
+#define OO_RES_MAX 0  // off by default: see OO_POLL_MAX below
 #endif
 constexpr uint32_t RES_WAVES = 32;
 static_assert(OO_RES_MAX <= 8 * RES_WAVES, "a resident batch is one 8-packet tile per wave at most");
@@ -140,7 +145,7 @@ static_assert(OO_RES_MAX <= 8 * RES_WAVES, "a resident batch is one 8-packet til
 constexpr uint64_t kResIdleTicks = 20000000ull;  // s_memrealtime, 100 MHz
 constexpr int64_t kResUsableNs = 100 * 1000 * 1000;
 #ifndef OO_POLL_MAX
-#define OO_POLL_MAX 256
+#define OO_POLL_MAX 0
 #endif
 #ifndef OO_POLL_DONE_MAX
 #define OO_POLL_DONE_MAX 2048

@@ -71,9 +71,10 @@ def test_poll_dispatch_and_counters(cuda, sw_verify, evs_per_poll, seed):
         assert a == b, (k, a, b)
     st = p.stats.as_dict()
     assert onload_stats(st) == want
-    if evs_per_poll in (64, 200):  # chunks the resident poll kernel takes once it runs
-        rs = g.resident_stats()
-        assert rs["batches"] > 0 and rs["fallbacks"] == 0 and rs["instances"] >= 1, rs
+    rs = g.resident_stats()
+    if rs["instances"]:  # a library built with the resident poll kernel on
+        assert evs_per_poll > 200 or rs["batches"] > 0, rs
+        assert rs["fallbacks"] == 0, rs
     ntrans = len(want_recs)
     assert st["n_batches"] == (0 if ntrans == 0 else
                                sum(1 for s in range(0, len(evs), evs_per_poll)
