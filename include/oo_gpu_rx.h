@@ -235,10 +235,10 @@ uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* ctx);
 /* Which kernels transformed the context's last batch: 1 rx_kernel with the
  * 4-slot ring, 2 its 2-slot instance, 3 the split transform (win_kernel +
  * body_kernel with lockstep slots), 4 the split transform with the
- * per-group-sequence body_kernel, 5 the poll instance (12-slot ring: path
- * 4, or in a library built with OO_POLL_MAX=256 batches of at most 256
- * packets), 6 the resident poll kernel (the same tile loop, no launch; in a
- * library built with OO_RES_MAX=256); 0 none yet.  For measurements: which
+ * per-group-sequence body_kernel, 5 the poll instance (12-slot ring; only
+ * in a library built with OO_POLL_MAX=256: path 4, and batches of at most
+ * 256 packets), 6 the resident poll kernel (the same tile loop, no launch; in
+ * a library built with OO_RES_MAX=256); 0 none yet.  For measurements: which
  * kernels a timed launch's duration covers. */
 uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* ctx);
 /* Table maintenance so far: flushes of queued changes to the device, and how
@@ -323,7 +323,8 @@ typedef struct oo_gpu_rx_tuning {
                               2 the same with the 2-slot ring; 3 the split
                               transform (win_kernel + body_kernel); 4 the
                               poll instance (12-slot ring; a submit_mapped
-                              batch's completion written by the kernel)    */
+                              batch's completion written by the kernel) in
+                              a library built with it, else as 1           */
   uint32_t grid_pct;       /* % of the resident grid to launch (0: 100)       */
   uint32_t groups;         /* tile-claim groups at most (0: by frame size)    */
   int32_t  gshift;         /* a group's wave runs, log2 (-1: by frame size)   */

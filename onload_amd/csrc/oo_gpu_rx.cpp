@@ -126,11 +126,12 @@ constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 K
 constexpr uint32_t SMALL_N = 2048;    // launch(): batches up to this many packets take 8-packet tiles
 // The poll instance (auto) up to OO_POLL_MAX packets, writing a
 // submit_mapped batch's done word itself up to OO_POLL_DONE_MAX (build-time
-// knobs for same-box A/Bs: tools/poll_ab.sh).  Off by default (0; the tuning
-// path 4 still forces it): every process in which the GPU faulted this round
-// had run it, none before it went in; the cause is
-// not found.  Built with OO_POLL_MAX=256 OO_RES_MAX=256 (make poll-variants:
-// pollres) it takes a poll's batches, and the resident kernel those of
+// knobs for same-box A/Bs: tools/poll_ab.sh).  Not in the product build
+// (OO_POLL_INSTANCE 0: no launch of it at all, the tuning path 4 runs
+// rx_kernel): every process in which the GPU faulted this round had run it,
+// none before it went in; the cause is not found.
+// Built with OO_POLL_MAX=256 OO_RES_MAX=256 (make poll-variants: pollres) it
+// takes a poll's batches, and the resident kernel those of
 // oo_gpu_rx_submit_mapped.
 // The resident poll kernel (oo_rx_kernel.hip "The resident poll kernel")
 // takes submit_mapped batches of at most OO_RES_MAX packets (0: never) once
@@ -146,6 +147,9 @@ constexpr uint64_t kResIdleTicks = 20000000ull;  // s_memrealtime, 100 MHz
 constexpr int64_t kResUsableNs = 100 * 1000 * 1000;
 #ifndef OO_POLL_MAX
 #define OO_POLL_MAX 0
+#endif
+#ifndef OO_POLL_INSTANCE
+#define OO_POLL_INSTANCE (OO_POLL_MAX > 0 || OO_RES_MAX > 0)
 #endif
 #ifndef OO_POLL_DONE_MAX
 #define OO_POLL_DONE_MAX 2048
@@ -936,7 +940,7 @@ void apply_tuning(oo_gpu_rx_ctx* c, const oo_gpu_rx_tuning* t) {
   c->grid_win = grid(c->bpc[2]);
   c->grid_body = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[3]) : c->bpc[3]);
   c->grid_body_gseq = grid(t->body_bpc ? std::min(t->body_bpc, c->bpc[4]) : c->bpc[4]);
-  c->grid_poll = grid(c->bpc[5]);
+  c->grid_poll = OO_POLL_INSTANCE ? grid(c->bpc[5]) : 0u;
   c->body_engine = t->body_engine;
   c->kx = t->walks == 0;
   c->kmode = t->path;

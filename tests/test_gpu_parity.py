@@ -236,14 +236,13 @@ def test_tile_partitions_and_claim_reuse(cuda, env, monkeypatch):
     g.close()
 
 
-@pytest.mark.parametrize("kernel", ["1", "2", "3", "3:1", "3:2", "4"])
+@pytest.mark.parametrize("kernel", ["1", "2", "3", "3:1", "3:2"])
 def test_both_rx_kernels_on_every_corpus(cuda, kernel, monkeypatch):
     """The 4-slot-ring rx_kernel (long frames) and the 2-slot one (short
     frames, 12 waves per CU) are chosen per launch by buffer bytes per packet
     (oo_gpu_rx.cpp launch()); forced here (OO_RX_KERNEL 1 / 2, and 3: the
     split transform, win_kernel + body_kernel; 3:1 / 3:2 with its lockstep
-    or per-group-sequence body engine forced; 4: the poll instance, 12-slot
-    ring, on batches of every size), each must be
+    or per-group-sequence body engine forced), each must be
     bit-exact on the edge corpus at odd and even alignments and on samples of
     every configuration, with several launches per context."""
     kernel, _, engine = kernel.partition(":")  # 3:E -- the split with body engine E

@@ -45,8 +45,8 @@ def _oracle_records(frames, evs, pool, sw_verify):
 @pytest.mark.parametrize("sw_verify,evs_per_poll,seed", [(1, 64, 1), (1, 1000, 2), (0, 64, 3),
                                                          (1, 1, 4), (1, 200, 5)])
 def test_poll_dispatch_and_counters(cuda, sw_verify, evs_per_poll, seed):
-    # (chunks of 64 and 200: the poll instance, descriptors in the kernel
-    # arguments up to 128 and read from the chunk beyond; 1000: rx_kernel)
+    # (chunks of 64 and 200: 8-packet tiles -- the poll instance in a library
+    # built with it; 1000: rx_kernel's 64-packet tiles)
     rng = np.random.default_rng(seed)
     frames = edge_frames(seed=seed)
     if evs_per_poll == 1:
