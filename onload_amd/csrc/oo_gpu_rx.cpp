@@ -156,6 +156,10 @@ constexpr int64_t kResUsableNs = 100 * 1000 * 1000;
 #endif
 constexpr int NTRACK = 8;             // streams tracked at once (LRU)
 constexpr int NSLOT = 2;              // host-path staging slots (double buffering)
+// Host words the device writes and the host polls (done words, the length
+// sample, the key index's rebuild request): fine-grained, so the GPU does not
+// hold them in its L2 -- they are freed with the context.
+constexpr unsigned kGpuWritten = hipHostMallocMapped | hipHostMallocCoherent;
 // Tile-claim counter sets: two per tracked stream (its launches alternate
 // between them), oo_rx::CLAIM_LINES lines of 128 B each (both kernels' group
 // counters and the body flag).
@@ -187,7 +191,6 @@ struct Tracked {
 // the kernel that read it has finished (ev).
 struct OpStage {
   TableOp* h = nullptr;
-  TableOp* hd = nullptr;  // h as the device addresses it (small flushes read it in place)
   TableOp* d = nullptr;
   hipEvent_t ev = nullptr;
   bool pending = false;
@@ -797,9 +800,8 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
   for (uint32_t i = 0; i < total; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(),
                    [c](uint32_t a, uint32_t b) { return c->op_level[a] < c->op_level[b]; });
-  // A small flush: the kernel reads the ops from the pinned staging buffer
-  // itself (no copy on the stream) and, with filter ops only and the index
-  // not asking for a rebuild, updates the index for the ops' keys.
+  // A small flush with filter ops only and the index not asking for a
+  // rebuild updates the index for the ops' keys.
   const bool small = total <= oo_table_threads();
   const bool req = c->h_kx_req != nullptr && *reinterpret_cast<volatile uint32_t*>(c->h_kx_req) != 0;
   const bool inc = small && !c->kx_full && !c->ops_sock && !req && c->d_kx_req != nullptr &&
@@ -823,17 +825,14 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
     }
     lev_end[nlev++] = n;
     if (inc) mark_kx_owners(h, n);
+    // (Copied to device memory even when small: the kernel does not read
+    // host memory in place -- DESIGN.md §5 round 5, the faults.)
     const TableOp* d_ops = st.d;
     const uint32_t* d_lev = reinterpret_cast<const uint32_t*>(st.d + OPS_CHUNK);
-    bool ok = true;
-    if (small && st.hd != nullptr) {
-      d_ops = st.hd;
-      d_lev = reinterpret_cast<const uint32_t*>(st.hd + OPS_CHUNK);
-    } else {
-      ok = hipMemcpyAsync(st.d, st.h, sizeof(TableOp) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
-           hipMemcpyAsync(st.d + OPS_CHUNK, lev_end, sizeof(uint32_t) * nlev, hipMemcpyHostToDevice,
-                          s) == hipSuccess;
-    }
+    const bool ok =
+        hipMemcpyAsync(st.d, st.h, sizeof(TableOp) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
+        hipMemcpyAsync(st.d + OPS_CHUNK, lev_end, sizeof(uint32_t) * nlev, hipMemcpyHostToDevice, s) ==
+            hipSuccess;
     if (!ok || oo_table_launch_ops(&c->T, d_ops, d_lev, nlev, c->gen, inc ? 1u : 0u, c->d_kx_req, s) != 0 ||
         hipEventRecord(st.ev, s) != hipSuccess) {
       c->failed = true;  // this chunk or an earlier one may have reached the device
@@ -917,7 +916,7 @@ int alloc_host_slots(oo_gpu_rx_ctx* c) {
         hipHostMalloc(&s.h_desc, sizeof(oo_gpu_pkt_desc) * pk, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&s.h_out, sizeof(oo_gpu_rx_result) * pk, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&s.h_ctr, sizeof(oo_gpu_rx_counters), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&s.h_done, 128, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.h_done, 128, kGpuWritten) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&s.d_done), s.h_done, 0) != hipSuccess)
       return -ENOMEM;
     *s.h_done = 0;
@@ -1049,13 +1048,12 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   for (OpStage& st : c->stage)
     ok = ok && hipHostMalloc(&st.h, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK,
                              hipHostMallocDefault) == hipSuccess &&
-         hipHostGetDevicePointer(reinterpret_cast<void**>(&st.hd), st.h, 0) == hipSuccess &&
          hipMalloc(&st.d, (sizeof(TableOp) + sizeof(uint32_t)) * OPS_CHUNK) == hipSuccess &&
          hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipHostMalloc(&c->h_len, 128, hipHostMallocDefault) == hipSuccess &&
+  ok = ok && hipHostMalloc(&c->h_len, 128, kGpuWritten) == hipSuccess &&
        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_len), c->h_len, 0) == hipSuccess &&
        hipEventCreateWithFlags(&c->len_ev, hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipHostMalloc(&c->h_kx_req, 128, hipHostMallocDefault) == hipSuccess &&
+  ok = ok && hipHostMalloc(&c->h_kx_req, 128, kGpuWritten) == hipSuccess &&
        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_kx_req), c->h_kx_req, 0) == hipSuccess;
   if (ok) *c->h_kx_req = 0;
   if (ok && cfg->host_stage_bytes && cfg->host_stage_pkts) {

@@ -36,7 +36,7 @@ print(sys.argv[1].split("/")[-1], d["value"], r["kernel_ms"], r["frac"], r.get("
 for step in ${STEPS:-tests bench}; do
   case $step in
     tests)
-      AMD_LOG_LEVEL=1 timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 120 \
+      AMD_LOG_LEVEL=${HIP_LOG:-1} timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 120 \
         --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} > "$OUT/gpu_tests.log" 2>&1 \
         || fail tests $? "$OUT/gpu_tests.log"
       tail -2 "$OUT/gpu_tests.log" ;;
