@@ -22,6 +22,7 @@
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 enum { W_TRANSFORM = 0, W_RELEASE = 1, W_OTHER = 2 };
 
@@ -62,13 +63,26 @@ static uint32_t be32_at(const uint8_t* p)
   return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
 }
 
-static void* alloc64(uint64_t bytes)
+/* The buffers the device maps (descriptors, records, gathered frames):
+ * whole pages of their own, from mmap, so no other allocation of the
+ * process ever shares a page with a registered range (DESIGN.md §5 round 5,
+ * the faults).  Zeroed. */
+static uint64_t page_bytes(uint64_t bytes)
 {
-  void* p = NULL;
-  if( posix_memalign(&p, 4096, bytes ? bytes : 64) != 0 )
-    return NULL;
-  memset(p, 0, bytes ? bytes : 64);
-  return p;
+  return ((bytes ? bytes : 1) + 4095) & ~(uint64_t)4095;
+}
+
+static void* alloc_pages(uint64_t bytes)
+{
+  void* p = mmap(NULL, page_bytes(bytes), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS,
+                 -1, 0);
+  return p == MAP_FAILED ? NULL : p;
+}
+
+static void free_pages(void* p, uint64_t bytes)
+{
+  if( p != NULL )
+    munmap(p, page_bytes(bytes));
 }
 
 /* Registers p with the device; 1 and *d set on success. */
@@ -85,9 +99,9 @@ static void chunk_free(oo_rx_poll* p, struct chunk* c)
     oo_gpu_rx_host_unregister(p->gpu, c->rec);
   if( c->d_pack )
     oo_gpu_rx_host_unregister(p->gpu, c->pack);
-  free(c->pack);
-  free(c->desc);
-  free(c->rec);
+  free_pages(c->pack, p->pack_bytes);
+  free_pages(c->desc, sizeof(oo_gpu_pkt_desc) * (uint64_t)p->cfg.evs_per_poll);
+  free_pages(c->rec, sizeof(oo_gpu_rx_result) * (uint64_t)p->cfg.evs_per_poll);
   free(c->ev_of);
   free(c->what);
 }
@@ -110,12 +124,12 @@ void oo_rx_poll_close(oo_rx_poll* p)
 static int chunk_alloc(oo_rx_poll* p, struct chunk* c)
 {
   const uint32_t n = p->cfg.evs_per_poll;
-  c->desc = alloc64(sizeof(oo_gpu_pkt_desc) * (uint64_t)n);
-  c->rec = alloc64(sizeof(oo_gpu_rx_result) * (uint64_t)n);
+  c->desc = alloc_pages(sizeof(oo_gpu_pkt_desc) * (uint64_t)n);
+  c->rec = alloc_pages(sizeof(oo_gpu_rx_result) * (uint64_t)n);
   c->ev_of = malloc(sizeof(uint32_t) * (uint64_t)n);
   c->what = malloc(n);
   if( !p->zero_copy )
-    c->pack = alloc64(p->pack_bytes);
+    c->pack = alloc_pages(p->pack_bytes);
   if( !c->desc || !c->rec || !c->ev_of || !c->what || (!p->zero_copy && !c->pack) )
     return -ENOMEM;
   return 0;
@@ -173,7 +187,7 @@ int oo_rx_poll_open(oo_rx_poll** out, oo_gpu_rx_ctx* gpu, const oo_rx_poll_cfg* 
     p->d_pool = NULL;
     p->zero_copy = 0;
     for( i = 0; i < 2; ++i )
-      if( (p->ch[i].pack = alloc64(p->pack_bytes)) == NULL ) {
+      if( (p->ch[i].pack = alloc_pages(p->pack_bytes)) == NULL ) {
         oo_rx_poll_close(p);
         return -ENOMEM;
       }

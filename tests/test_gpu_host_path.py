@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 from gpu_util import diff_report, run_dev
+from hostmem import page_buffer
 from onload_amd import _abi, pktgen
 from onload_amd.rx import GpuRxStack
 from oracle_lib import OracleStack, counters_of
@@ -34,11 +35,9 @@ def cuda():
 
 
 def aligned(nbytes: int, dtype=np.uint8) -> np.ndarray:
-    """A page-aligned host array (hipHostRegister works on whole pages)."""
-    item = np.dtype(dtype).itemsize
-    raw = np.zeros(nbytes * item + 2 * PAGE, dtype=np.uint8)
-    off = (-raw.ctypes.data) % PAGE
-    return raw[off: off + nbytes * item].view(dtype)
+    """A host array on pages of its own (hostmem.page_buffer: hipHostRegister
+    works on whole pages)."""
+    return page_buffer(nbytes, dtype)
 
 
 def test_submit_wait_pageable_matches_device_path(cuda):

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 from frames import edge_frames, edge_world, install, pack
+from hostmem import page_buffer
 from onload_amd import _abi, poll
 from onload_amd.rx import GpuRxStack
 from oracle_lib import OracleStack
@@ -98,7 +99,7 @@ def test_poll_stage_routing(cuda):
     g = GpuRxStack(device=0, host_stage_bytes=1 << 20, host_stage_pkts=1024)
     install(g, (socks, filters))
     f = cases.order_frame()
-    pool = np.zeros(4 * 2048, np.uint8)
+    pool = page_buffer(4 * 2048)
     pool[192:192 + len(f)] = np.frombuffer(f, np.uint8)
     ev = np.zeros(1, poll.EV_DTYPE)
     ev[0] = (0, 192, len(f), poll.EV_SOP, 0, 0, 0)
@@ -194,7 +195,7 @@ def test_poll_table_change_in_a_callback(cuda, evs_per_poll):
     install(g, (socks, filters))
     f = cases.order_frame()
     n = 4 * evs_per_poll
-    pool = np.zeros(n * 2048, np.uint8)
+    pool = page_buffer(n * 2048)
     evs = np.zeros(n, poll.EV_DTYPE)
     for i in range(n):
         pool[i * 2048 + 192:i * 2048 + 192 + len(f)] = np.frombuffer(f, np.uint8)
@@ -288,7 +289,7 @@ def test_poll_table_change_then_rest_handed_back(cuda):
     f = cases.order_frame()
     epp = 64
     n = 3 * epp
-    pool = np.zeros(n * 2048, np.uint8)
+    pool = page_buffer(n * 2048)
     evs = np.zeros(n, poll.EV_DTYPE)
     for i in range(n):
         pool[i * 2048 + 192:i * 2048 + 192 + len(f)] = np.frombuffer(f, np.uint8)
