@@ -411,8 +411,11 @@ int oo_gpu_rx_xdp_poll(oo_gpu_rx_ctx* ctx, const void* d_umem, uint64_t umem_byt
  * result arrays.  *dev_ptr (may be NULL) receives the device address of p,
  * for oo_gpu_rx_xdp_dev / _poll (zero-copy ingest) or process_dev.
  * Registered frames, descriptors and results skip the pinned staging copy
- * of oo_gpu_rx_submit.  0, -EINVAL, -ENOMEM, -ENODEV.  unregister: 0 or
- * -ENOENT (p must be a registered base); waits for the context's batches. */
+ * of oo_gpu_rx_submit.  Register whole pages that no other allocation
+ * shares (an mmap'd or huge-page pool, as Onload's is): the registration
+ * pins and maps whole pages.  0, -EINVAL, -ENOMEM, -ENODEV.  unregister: 0
+ * or -ENOENT (p must be a registered base); waits for the context's
+ * batches. */
 int oo_gpu_rx_host_register(oo_gpu_rx_ctx* ctx, void* p, uint64_t bytes, void** dev_ptr);
 int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* ctx, void* p);
 
