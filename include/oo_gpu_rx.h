@@ -254,8 +254,8 @@ typedef struct oo_gpu_rx_table_stats {
   uint32_t rsvd;
 } oo_gpu_rx_table_stats;
 int oo_gpu_rx_get_table_stats(oo_gpu_rx_ctx* ctx, oo_gpu_rx_table_stats* out);
-/* The resident poll kernel (built in with OO_RES_MAX=256,
- * off by default): a context that submits
+/* The resident poll kernel (only in a library built with
+ * OO_POLL_MAX=256 OO_RES_MAX=256, not the product build): a context that submits
  * oo_gpu_rx_submit_mapped batches of at most 256 packets starts a small
  * grid that stays on the device and takes them from a doorbell in host
  * memory, with no launch per batch; it leaves after 200 ms without one (and

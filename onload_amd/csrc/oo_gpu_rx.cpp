@@ -137,7 +137,7 @@ constexpr uint32_t SMALL_N = 2048;    // launch(): batches up to this many packe
 // takes submit_mapped batches of at most OO_RES_MAX packets (0: never) once
 // it runs; OO_RES_WAVES waves, a tile of eight packets each.
 #ifndef OO_RES_MAX
-#define OO_RES_MAX 0  // off by default: see OO_POLL_MAX below
+#define OO_RES_MAX 0  // not in the product build: see OO_POLL_MAX below
 #endif
 constexpr uint32_t RES_WAVES = 32;
 static_assert(OO_RES_MAX <= 8 * RES_WAVES, "a resident batch is one 8-packet tile per wave at most");
