@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU-box driver for a round's measurements (run through gpurun from the
 # repo root).  Steps, in the order given in STEPS (default "tests bench"):
-#   tests     the -m gpu suite (TESTS files, TESTS_K -k filter) -> gpu_tests.log
+#   tests     the -m gpu suite (TESTS files, TESTS_K -k filter; HIP_LOG sets
+#             AMD_LOG_LEVEL, default 1: HIP's errors) -> gpu_tests.log
 #   smoke     __graft_entry__.smoke()
 #   bench     the driver-shaped bench line (--steps 20 --warmup 5) per config in
 #             CONFIGS (config 2 with its cpu_baseline) -> bench_c<N>.json
