@@ -157,3 +157,45 @@ def test_zero_copy_umem_ring_poll(cuda):
     np.testing.assert_array_equal(ctr.cpu().numpy().astype(np.uint32), counters_of(want))
     g.host_unregister(ring)
     g.host_unregister(umem)
+
+
+@pytest.mark.parametrize("kernel", ["0", "1", "2", "3"])
+def test_frames_flush_with_registered_page_ends(cuda, kernel, monkeypatch):
+    """Frames read in place from registered host memory, each page holding
+    one frame from its first bytes (odd offset) and one ending at its last
+    byte -- the pool's last frame ends at the registration's last byte, and
+    the page after it is not mapped for the device.  Every kernel reads only
+    the lines that hold its frames' bytes, so no access leaves the
+    registered pages (one that did would fault the GPU); records equal the
+    oracle's."""
+    torch = cuda
+    monkeypatch.setenv("OO_RX_KERNEL", kernel)
+    filters, socks = pktgen.world(2)
+    g = GpuRxStack(device=0)
+    o = OracleStack()
+    for st in (g, o):
+        st.load_world(filters, socks)
+    buf0, desc0 = pktgen.generate(2, 8, first=4242)
+    frames = [bytes(buf0[int(d["frame_off"]):int(d["frame_off"]) + int(d["len"])]) for d in desc0]
+    frames[5] = frames[5][:61]  # a short capture among them
+    pages = 4
+    pool = page_buffer(pages * PAGE)
+    desc = np.zeros(2 * pages, _abi.DESC_DTYPE)
+    for p in range(pages):
+        for k, f in enumerate(frames[2 * p:2 * p + 2]):
+            off = p * PAGE + 3 if k == 0 else (p + 1) * PAGE - len(f)
+            pool[off:off + len(f)] = np.frombuffer(f, np.uint8)
+            desc[2 * p + k] = (off, len(f), 0, 0)
+    d_pool = g.host_register(pool)
+    de = torch.from_numpy(desc.view(np.uint8)).to("cuda")
+    out = torch.full((len(desc) * 32,), 0xAB, dtype=torch.uint8, device="cuda")
+    ctr = torch.zeros(_abi.R_COUNT, dtype=torch.int32, device="cuda")
+    g.handle_rx_batch_dev(d_pool, pool.nbytes, de.data_ptr(), len(desc), out.data_ptr(),
+                          ctr.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(_abi.RESULT_DTYPE)
+    want = o.handle_rx_batch(pool, desc, nthreads=1)
+    assert got.tobytes() == want.tobytes(), diff_report(got, want, desc)
+    np.testing.assert_array_equal(ctr.cpu().numpy().astype(np.uint32), counters_of(want))
+    g.host_unregister(pool)
+    g.close()
