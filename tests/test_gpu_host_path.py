@@ -199,3 +199,48 @@ def test_frames_flush_with_registered_page_ends(cuda, kernel, monkeypatch):
     np.testing.assert_array_equal(ctr.cpu().numpy().astype(np.uint32), counters_of(want))
     g.host_unregister(pool)
     g.close()
+
+
+def test_xdp_frames_and_ring_flush_with_registered_page_ends(cuda):
+    """The AF_XDP form of the page-end test: UMEM frames flush with the first
+    and last bytes of registered pages, the RX ring exactly one registered
+    page (256 entries, the batch wrapping its end), read in place by
+    oo_gpu_rx_xdp_poll; records equal the oracle's ring batch."""
+    torch = cuda
+    filters, socks = pktgen.world(2)
+    g = GpuRxStack(device=0)
+    o = OracleStack()
+    for st in (g, o):
+        st.load_world(filters, socks)
+    buf0, desc0 = pktgen.generate(2, 8, first=777)
+    frames = [bytes(buf0[int(d["frame_off"]):int(d["frame_off"]) + int(d["len"])]) for d in desc0]
+    pages = 4
+    umem = page_buffer(pages * PAGE)
+    ents = np.zeros(2 * pages, _abi.XDP_DESC_DTYPE)
+    for p in range(pages):
+        for k, f in enumerate(frames[2 * p:2 * p + 2]):
+            off = p * PAGE + 1 if k == 0 else (p + 1) * PAGE - len(f)
+            umem[off:off + len(f)] = np.frombuffer(f, np.uint8)
+            ents[2 * p + k] = (off, len(f), 0)
+    ring = page_buffer(PAGE // 16, _abi.XDP_DESC_DTYPE)
+    cons0 = 256 - 3
+    ring0, mask = ring_of(ents, 8, cons0)
+    ring[:] = ring0
+    n = len(ents)
+    d_umem = g.host_register(umem)
+    d_ring = g.host_register(ring)
+    want = o.handle_xdp_batch(umem, ring, mask, cons0, n, 1)
+    out = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    ctr = torch.zeros(_abi.R_COUNT, dtype=torch.int32, device="cuda")
+    consumer = np.array([cons0], dtype=np.uint32)
+    producer = np.array([cons0 + n], dtype=np.uint32)
+    k = g.xdp_poll(d_umem, umem.nbytes, d_ring, mask, consumer, producer, 64, 1,
+                   out.data_ptr(), ctr.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert k == n and int(consumer[0]) == cons0 + n
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(_abi.RESULT_DTYPE)
+    assert got.tobytes() == want.tobytes(), diff_report(got, want)
+    np.testing.assert_array_equal(ctr.cpu().numpy().astype(np.uint32), counters_of(want))
+    g.host_unregister(ring)
+    g.host_unregister(umem)
+    g.close()
