@@ -326,3 +326,35 @@ def test_poll_table_change_then_rest_handed_back(cuda):
     assert st["rx_evs"] == len([i for i in range(n) if i % 5 != 4 and i not in rest])
     p.close()
     g.close()
+
+
+@pytest.mark.parametrize("zero_copy", (False, True))
+def test_frames_flush_with_pool_page_ends(cuda, zero_copy):
+    """Every frame ends at its 2048-B buffer's last byte -- every second one
+    at a page's, the last at the registered pool's -- read in place (zero
+    copy) or gathered: the shim's batches never read past a frame's lines,
+    and the records the callbacks see are the oracle's."""
+    frames = [(f, i) for f, i in edge_frames(seed=11) if 0 < len(f) <= 2048]
+    n = len(frames)
+    pool = page_buffer(n * 2048)
+    evs = np.zeros(n, poll.EV_DTYPE)
+    for i, (f, intf) in enumerate(frames):
+        ofs = 2048 - len(f)
+        pool[i * 2048 + ofs:(i + 1) * 2048] = np.frombuffer(f, np.uint8)
+        evs[i] = (i, ofs, len(f), poll.EV_SOP, 0, intf, 0)
+    g = GpuRxStack(device=0, intf_hwport=HWPORTS, host_stage_bytes=16 << 20,
+                   host_stage_pkts=4096)
+    install(g, edge_world())
+    rec = Recorder(lambda i: False)
+    p = poll.RxPoll(g, pool, 2048, 64, True, rec, zero_copy=zero_copy)
+    assert p.poll(evs) == n
+    o = OracleStack(intf_hwport=HWPORTS)
+    install(o, edge_world())
+    sel = [frames[i] for i in range(n) if transformed(evs[i], True, 2048, pool.nbytes)]
+    buf, desc = pack(sel)
+    want = o.handle_rx_batch(buf, desc)
+    got = np.array([tuple(r[k] for k in _abi.RESULT_DTYPE.names) for r in rec.recs],
+                   dtype=_abi.RESULT_DTYPE)
+    assert len(sel) > 100 and got.tobytes() == want.tobytes()
+    p.close()
+    g.close()
