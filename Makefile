@@ -96,7 +96,8 @@ tools/poll_bench: tools/poll_bench.c $(SHIM) $(PKTGEN) oracle include/oo_rx_poll
 # Builds for tools/poll_ab.sh (build/pollvar/<name>/liboo_gpu_rx.so); not part
 # of `all`.
 POLL_VARIANTS ?= pollres:-DOO_POLL_MAX=256,-DOO_RES_MAX=256 \
-                  pollresinl:-DOO_POLL_MAX=256,-DOO_RES_MAX=256,-DOO_POLL_INLINE=128
+                  pollresinl:-DOO_POLL_MAX=256,-DOO_RES_MAX=256,-DOO_POLL_INLINE=128 \
+                  doneev:-DOO_DONE_EVENT=1
 poll-variants: $(SRCS) $(HDRS)
 	for v in $(POLL_VARIANTS); do n=$${v%%:*}; f=$$(echo "$${v#*:}" | tr ',' ' '); mkdir -p build/pollvar/$$n; \
 	  $(HIPCC) $(HIPFLAGS) $$f -shared -Wl,-soname,liboo_gpu_rx.so -o build/pollvar/$$n/liboo_gpu_rx.so $(SRCS) -ldl || exit 1; done

@@ -151,6 +151,11 @@ constexpr int64_t kResUsableNs = 100 * 1000 * 1000;
 #ifndef OO_POLL_INSTANCE
 #define OO_POLL_INSTANCE (OO_POLL_MAX > 0 || OO_RES_MAX > 0)
 #endif
+#ifndef OO_DONE_EVENT
+// 1: a host-path batch completes by its event alone (the waiter spins on
+// hipEventQuery) -- no stream-written done word (A/B knob, make poll-variants).
+#define OO_DONE_EVENT 0
+#endif
 #ifndef OO_POLL_DONE_MAX
 #define OO_POLL_DONE_MAX 2048
 #endif
@@ -1833,6 +1838,19 @@ static bool spin_done(const HostSlot& s) {
   }
 }
 
+// OO_DONE_EVENT: the slot's event polled instead (a runtime call per read).
+static bool spin_event(hipEvent_t e) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return true;
+    if (r != hipErrorNotReady ||
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                .count() > kSpinNs)
+      return false;
+  }
+}
+
 // A resident batch whose done word did not come: stop the instance (quit,
 // its stream drained), and unless it took the batch after all, run the
 // batch through the launch path on the slot's stream and wait for it
@@ -1850,7 +1868,7 @@ static int complete_slot(oo_gpu_rx_ctx* c, HostSlot& s) {
     s.busy = s.res = false;
     return (int)s.n;
   }
-  if (!spin_done(s) && hipEventSynchronize(s.done) != hipSuccess) {
+  if (!(OO_DONE_EVENT ? spin_event(s.done) : spin_done(s)) && hipEventSynchronize(s.done) != hipSuccess) {
     s.busy = false;
     return -EIO;
   }
@@ -1932,7 +1950,7 @@ int oo_gpu_rx_submit(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes
   }
   ok = ok && hipMemcpyAsync(s.h_ctr, s.d_ctr, sizeof(oo_gpu_rx_counters), hipMemcpyDeviceToHost,
                             st) == hipSuccess &&
-       hipStreamWriteValue32(st, s.d_done, done_word(t), 0) == hipSuccess &&
+       (OO_DONE_EVENT || hipStreamWriteValue32(st, s.d_done, done_word(t), 0) == hipSuccess) &&
        hipEventRecord(s.done, st) == hipSuccess;
   if (!ok) return -EIO;
   s.busy = true;
@@ -2026,7 +2044,7 @@ int oo_gpu_rx_submit_mapped(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t fra
     }
     if (rc) return rc;
   }
-  if ((!by_kernel && hipStreamWriteValue32(st, s.d_done, done_word(t), 0) != hipSuccess) ||
+  if ((!by_kernel && !OO_DONE_EVENT && hipStreamWriteValue32(st, s.d_done, done_word(t), 0) != hipSuccess) ||
       hipEventRecord(s.done, st) != hipSuccess)
     return -EIO;
   s.busy = true;
