@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import mmap
 import os
 import socket
 import subprocess
@@ -607,9 +608,10 @@ def time_xdp(torch, stack, buf, desc, ref_out, dev, sh, steps, warmup, headroom=
 
 
 def _pinned_aligned(nbytes):
-    raw = np.zeros(nbytes + 8192, dtype=np.uint8)
-    off = (-raw.ctypes.data) % 4096
-    return raw[off:off + nbytes]
+    """nbytes of host memory on whole pages of its own (an anonymous mmap,
+    unmapped when the array goes): what oo_gpu_rx_host_register takes."""
+    m = mmap.mmap(-1, max(1, -(-nbytes // mmap.PAGESIZE)) * mmap.PAGESIZE)
+    return np.frombuffer(m, dtype=np.uint8, count=nbytes)
 
 
 def time_xdp_host(torch, stack, buf, desc, ref_out, dev, sh, reps=5, headroom=192):

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OO_GPU_RX_ABI_VERSION 4
+#define OO_GPU_RX_ABI_VERSION 5
 
 /* intf_i -> hwport map size (CI_CFG_MAX_INTERFACES = 30,
  * src/include/ci/internal/transport_config_opt.h:29). */
@@ -183,10 +183,13 @@ typedef struct oo_gpu_rx_cfg {
 
 typedef struct oo_gpu_rx_ctx oo_gpu_rx_ctx;
 
-/* Library / context lifetime. */
-int  oo_gpu_rx_abi_version(void);
-int  oo_gpu_rx_open(oo_gpu_rx_ctx** ctx_out, const oo_gpu_rx_cfg* cfg);
-void oo_gpu_rx_close(oo_gpu_rx_ctx* ctx);
+/* Library / context lifetime.  close: 0, or -EBUSY while host memory is
+ * still registered with the context (oo_gpu_rx_host_register): the context
+ * stays open; the caller unregisters that memory -- before it unmaps or
+ * frees it -- and closes again.  NULL: 0. */
+int oo_gpu_rx_abi_version(void);
+int oo_gpu_rx_open(oo_gpu_rx_ctx** ctx_out, const oo_gpu_rx_cfg* cfg);
+int oo_gpu_rx_close(oo_gpu_rx_ctx* ctx);
 
 /* Filter tables.  Replaces ci_netif_filter_insert / _remove
  * (netif_table.c:436-503 -> ci_ip4_netif_filter_insert :323-406,
@@ -411,13 +414,22 @@ int oo_gpu_rx_xdp_poll(oo_gpu_rx_ctx* ctx, const void* d_umem, uint64_t umem_byt
  * result arrays.  *dev_ptr (may be NULL) receives the device address of p,
  * for oo_gpu_rx_xdp_dev / _poll (zero-copy ingest) or process_dev.
  * Registered frames, descriptors and results skip the pinned staging copy
- * of oo_gpu_rx_submit.  Register whole pages that no other allocation
- * shares (an mmap'd or huge-page pool, as Onload's is): the registration
- * pins and maps whole pages.  0, -EINVAL, -ENOMEM, -ENODEV.  unregister: 0
- * or -ENOENT (p must be a registered base); waits for the context's
- * batches. */
+ * of oo_gpu_rx_submit.
+ * The contract, enforced: whole pages -- p and bytes multiples of the page
+ * size -- that no other registration of the process (any context) holds;
+ * -EINVAL otherwise.  The memory stays mapped until it is unregistered:
+ * unregister first, then unmap or free it (a context holding registrations
+ * does not close, oo_gpu_rx_close).  Pages of the range should hold nothing
+ * the caller copies to or from the device as pageable memory (an mmap'd or
+ * huge-page pool, as Onload's is).  A host-only
+ * context keeps the same books (*dev_ptr = p).  0, -EINVAL, -ENOMEM,
+ * -ENODEV, -EIO.
+ * unregister: waits for the context's batches, then 0, -ENOENT (p is not a
+ * registered base of this context) or -EIO (the runtime refused: the range
+ * stays registered).  registered: the number of ranges the context holds. */
 int oo_gpu_rx_host_register(oo_gpu_rx_ctx* ctx, void* p, uint64_t bytes, void** dev_ptr);
 int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* ctx, void* p);
+int oo_gpu_rx_host_registered(const oo_gpu_rx_ctx* ctx);
 
 /* Asynchronous host-memory batch (the NIC ring -> socket path): enqueues the
  * H2D copy of frames and descriptors, the transform and the D2H copy of the
@@ -492,7 +504,27 @@ int  oo_gpu_rx_group_open(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg,
 int  oo_gpu_rx_group_rccl_id(void* id);
 int  oo_gpu_rx_group_join(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32_t rank,
                           uint32_t nranks, const void* id);
-void oo_gpu_rx_group_close(oo_gpu_rx_group* g);
+/* The join shape over a caller's transport instead of RCCL: a host-only
+ * member (cfg->device < 0, else -EINVAL) whose collectives move host memory
+ * through the four calls below -- the control plane's own channel between
+ * the processes of a stack, for replicating its tables without a GPU, and
+ * the harness that runs the collectives' sequencing with injected failures.
+ * Each call is collective over the nranks callers and returns 0 or -errno
+ * locally: bcast copies rank 0's `bytes` at p to every rank's p; max_u32 /
+ * sum_u32 reduce n words in place; gather moves every rank's `bytes` at src
+ * to rank 0's dst in rank order (bytes_of[k]: rank k's bytes, the same on
+ * every rank). */
+typedef struct oo_gpu_rx_group_transport {
+  void* arg;
+  int (*bcast)(void* arg, void* p, uint64_t bytes);
+  int (*max_u32)(void* arg, uint32_t* v, uint32_t n);
+  int (*sum_u32)(void* arg, uint32_t* v, uint32_t n);
+  int (*gather)(void* arg, const void* src, uint64_t bytes, void* dst, const uint64_t* bytes_of);
+} oo_gpu_rx_group_transport;
+int  oo_gpu_rx_group_join_transport(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32_t rank,
+                                    uint32_t nranks, const oo_gpu_rx_group_transport* t);
+/* 0, or -EBUSY (nothing closed) while a member holds registered host memory. */
+int  oo_gpu_rx_group_close(oo_gpu_rx_group* g);
 /* Local members, this process's rank (0 in one process), member i's context
  * (its own calls -- export, sync_tables, stream_done -- work as for any
  * context; table changes go through the group). */
@@ -531,11 +563,16 @@ int oo_gpu_rx_group_gather(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards,
  * by the others in order (returns how many; -EIO on every rank when a
  * replica's return code differs from rank 0's or rank 0 lost a change, and
  * the caller then shares the tables again); every rank's n records to
- * rank 0's d_dst in rank order (rank 0 passes counts[nranks], counts[0] ==
- * its own n); the device counters summed on every rank.  Each call enters
- * all of its collectives on every rank and reports a local failure after
- * them (the staging they use is allocated at the join).  A joined group of
- * one rank runs the same RCCL calls. */
+ * rank 0's d_dst in rank order (rank 0 passes counts[nranks]; a count
+ * that differs from its rank's n, or rank 0 without d_dst / counts, is
+ * -EINVAL on every rank and moves nothing); the device counters summed on
+ * every rank.  Each call enters all of its collectives on every rank: where
+ * a local failure would leave a rank out of the next one, every rank first
+ * agrees on it (a one-word maximum) and all return the error together;
+ * later local failures are reported after the last collective.  The
+ * staging they use is allocated at the join.  A joined group of one rank
+ * runs the same RCCL calls.  A failure of the agreement itself (-EIO)
+ * means the communicator is unusable: close the group. */
 int oo_gpu_rx_group_share_tables(oo_gpu_rx_group* g, void* stream);
 int oo_gpu_rx_group_share_ops(oo_gpu_rx_group* g, void* stream);
 int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_out, uint32_t n,

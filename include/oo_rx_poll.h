@@ -197,8 +197,10 @@ typedef struct oo_rx_poll_cfg {
 } oo_rx_poll_cfg;
 
 /* cfg.flags: register pkt_bufs with the device and read frames in place
- * (falls back to gathering if the pool cannot be registered; see
- * oo_rx_poll_zero_copy). */
+ * (falls back to gathering if the pool cannot be registered -- it must be
+ * whole pages no other registration holds, oo_gpu_rx_host_register; see
+ * oo_rx_poll_zero_copy).  The shim unregisters it at oo_rx_poll_close, which
+ * must come before the context's close and before the pool is unmapped. */
 #define OO_RX_POLL_ZERO_COPY 0x1u
 /* cfg.flags: a chunk whose device batch would cost more than the caller's
  * own per-event path (the cost model above) is not transformed: all its

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboo_gpu_rx.so")
 PKTGEN_PATH = os.path.join(_HERE, "liboo_pktgen.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_INTF = 32
 
 # Reason codes (oo_gpu_rx.h), in the reference's check order.
@@ -159,7 +159,7 @@ _P, _U8, _U16, _U32, _U64, _I32 = (ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uin
 ABI_SYMBOLS = {
     "oo_gpu_rx_abi_version": (ctypes.c_int, []),
     "oo_gpu_rx_open": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(Cfg)]),
-    "oo_gpu_rx_close": (None, [_P]),
+    "oo_gpu_rx_close": (ctypes.c_int, [_P]),
     "oo_gpu_rx_table_insert": (ctypes.c_int, [_P, ctypes.c_int, _P, _U16, _P, _U16, _U8, _I32]),
     "oo_gpu_rx_table_remove": (ctypes.c_int, [_P, ctypes.c_int, _P, _U16, _P, _U16, _U8, _I32]),
     "oo_gpu_rx_table_lookup": (ctypes.c_int, [_P, ctypes.c_int, _P, _U16, _P, _U16, _U8]),
@@ -186,6 +186,7 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_submit_mapped": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, ctypes.POINTER(_U64)]),
     "oo_gpu_rx_host_register": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_P)]),
     "oo_gpu_rx_host_unregister": (ctypes.c_int, [_P, _P]),
+    "oo_gpu_rx_host_registered": (ctypes.c_int, [_P]),
     "oo_gpu_rx_table_image_bytes": (_U64, [_P]),
     "oo_gpu_rx_table_export": (ctypes.c_int, [_P, _P, _U64, _P]),
     "oo_gpu_rx_table_import": (ctypes.c_int, [_P, _P, _U64, _P]),
@@ -203,7 +204,9 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_group_rccl_id": (ctypes.c_int, [_P]),
     "oo_gpu_rx_group_join": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(Cfg), _U32, _U32,
                                             _P]),
-    "oo_gpu_rx_group_close": (None, [_P]),
+    "oo_gpu_rx_group_join_transport": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(Cfg),
+                                                      _U32, _U32, _P]),
+    "oo_gpu_rx_group_close": (ctypes.c_int, [_P]),
     "oo_gpu_rx_group_size": (_U32, [_P]),
     "oo_gpu_rx_group_rank": (_U32, [_P]),
     "oo_gpu_rx_group_member": (_P, [_P, _U32]),

@@ -22,10 +22,13 @@
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <map>
+#include <mutex>
 #include <new>
 #include <unordered_map>
 #include <unordered_set>
@@ -234,6 +237,18 @@ struct HostReg {
   uintptr_t lo, hi;
   void* dev;
 };
+
+// Every range registered by any context of the process, by first byte: a
+// registration is whole pages that no other registration shares
+// (oo_gpu_rx_host_register; DESIGN.md §5 round 6, the registration faults).
+std::mutex g_reg_mu;
+std::map<uintptr_t, uintptr_t> g_reg_pages;  // lo -> hi
+
+bool reg_overlaps(uintptr_t lo, uintptr_t hi) {
+  auto it = g_reg_pages.lower_bound(lo);
+  if (it != g_reg_pages.end() && it->first < hi) return true;
+  return it != g_reg_pages.begin() && std::prev(it)->second > lo;
+}
 
 }  // namespace
 
@@ -693,7 +708,6 @@ void free_dev(oo_gpu_rx_ctx* c) {
     if (t.pend) (void)hipFree(t.pend);
   }
   for (void* p : c->retired) (void)hipFree(p);
-  for (const HostReg& r : c->regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.lo));
   if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
   if (c->res_s) (void)hipStreamDestroy(c->res_s);
   if (c->h_mail) (void)hipHostFree(c->h_mail);
@@ -1077,17 +1091,24 @@ int oo_gpu_rx_open(oo_gpu_rx_ctx** out, const oo_gpu_rx_cfg* cfg) {
   return 0;
 }
 
-void oo_gpu_rx_close(oo_gpu_rx_ctx* c) {
-  if (c == nullptr) return;
+// A context with host memory still registered stays open (-EBUSY): only
+// the caller knows when that memory stops being mapped, so the caller
+// unregisters it -- before releasing it -- and closes again.  Unregistering
+// it here, after the caller may have freed or remapped those pages, is the
+// lifetime the round-5 faults pointed at.
+int oo_gpu_rx_close(oo_gpu_rx_ctx* c) {
+  if (c == nullptr) return 0;
+  if (!c->regs.empty()) return -EBUSY;
   if (!has_dev(c)) {
     delete c;
-    return;
+    return 0;
   }
   (void)hipSetDevice(c->device);
   if (c->h_bell != nullptr) __atomic_store_n(c->h_bell, oo_rx::RES_QUIT, __ATOMIC_RELEASE);
   (void)hipDeviceSynchronize();  // every stream the context launched on (the resident kernel has left)
   free_dev(c);
   delete c;
+  return 0;
 }
 
 int oo_gpu_rx_table_insert(oo_gpu_rx_ctx* c, int af, const void* laddr, uint16_t lport,
@@ -1671,25 +1692,47 @@ int oo_gpu_tx_fill_dev(oo_gpu_rx_ctx* c, void* d_frames, uint64_t frames_bytes,
                 static_cast<hipStream_t>(stream), true);
 }
 
+// Whole pages only, and none another registration of the process holds:
+// the contract Onload's own pools meet (efhw/af_xdp.c:463-500 pins whole
+// UMEM pages).  The runtime pins and maps whole pages and looks a host
+// address up among the registered ranges when it copies pageable memory, so
+// a page shared between two registrations, or between a registration and
+// memory the caller hands to other copies, is what DESIGN.md §5 round 6
+// names as the fault's condition.  The check and the record are one step
+// under the process-wide lock.
 int oo_gpu_rx_host_register(oo_gpu_rx_ctx* c, void* p, uint64_t bytes, void** dev_ptr) {
   if (c == nullptr || p == nullptr || bytes == 0) return -EINVAL;
-  if (!has_dev(c)) return -ENODEV;
-  if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
-  if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) return -ENOMEM;
-  void* d = nullptr;
-  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
-    (void)hipHostUnregister(p);
-    return -EIO;
-  }
+  const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
   const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+  if (lo % page != 0 || bytes % page != 0 || lo + bytes < lo) return -EINVAL;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  if (reg_overlaps(lo, lo + bytes)) return -EINVAL;
+  // A host-only context keeps the same books (its "device" address of p is
+  // p): the contract holds, and is testable, without a GPU.
+  const bool dev = has_dev(c);
+  void* d = p;
+  if (dev) {
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) return -ENOMEM;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+      (void)hipHostUnregister(p);
+      return -EIO;
+    }
+  }
   try {
     c->regs.push_back(HostReg{lo, lo + bytes, d});
+    g_reg_pages[lo] = lo + bytes;
   } catch (...) {
-    (void)hipHostUnregister(p);
+    if (!c->regs.empty() && c->regs.back().lo == lo) c->regs.pop_back();
+    if (dev) (void)hipHostUnregister(p);
     return -ENOMEM;
   }
   if (dev_ptr) *dev_ptr = d;
   return 0;
+}
+
+int oo_gpu_rx_host_registered(const oo_gpu_rx_ctx* c) {
+  return c == nullptr ? -EINVAL : (int)c->regs.size();
 }
 
 int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
@@ -1697,6 +1740,12 @@ int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
   const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
   for (size_t i = 0; i < c->regs.size(); ++i) {
     if (c->regs[i].lo != lo) continue;
+    if (!has_dev(c)) {
+      std::lock_guard<std::mutex> lk(g_reg_mu);
+      g_reg_pages.erase(lo);
+      c->regs.erase(c->regs.begin() + (long)i);
+      return 0;
+    }
     (void)hipSetDevice(c->device);
     // No batch may still read it.
     for (HostSlot& s : c->slot) {
@@ -1716,7 +1765,11 @@ int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
       hipEvent_t e = t.live ? mark(t) : t.ev;
       if (e != nullptr) (void)hipEventSynchronize(e);
     }
-    (void)hipHostUnregister(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    // A failed unregister leaves the range registered (and the context
+    // unclosable): its pages may still be mapped for the device.
+    if (hipHostUnregister(p) != hipSuccess) return -EIO;
+    g_reg_pages.erase(lo);
     c->regs.erase(c->regs.begin() + (long)i);
     return 0;
   }

@@ -110,17 +110,40 @@ constexpr uint32_t kOpsLost = 1;  // rank 0 could not queue an op: re-share the 
 
 }  // namespace
 
+// The join shape's collectives, on host words or on the group's data
+// memory (device memory over RCCL; host memory over a caller transport).
+// Every method enters its collective on every rank, whatever failed before
+// it locally, and reports a local failure by its return code.
+struct Xport {
+  virtual ~Xport() {}
+  // rank 0's `bytes` at host address h to every rank's h (bytes <= the
+  // op staging: kOpsHdr + one chunk)
+  virtual int bcast_words(void* h, uint64_t bytes) = 0;
+  // element-wise maximum over the ranks of n host words, in place
+  virtual int max_words(uint32_t* h, uint32_t n) = 0;
+  // rank 0's image at the group's staging p to every rank's
+  virtual int bcast_image(void* p, uint64_t bytes) = 0;
+  // every rank's `bytes` at src to rank 0's dst in rank order (bytes_of:
+  // every rank's bytes, known to every rank)
+  virtual int gather(const void* src, uint64_t bytes, void* dst, const uint64_t* bytes_of) = 0;
+  // the per-reason counters at p summed over the ranks, in place
+  virtual int sum_counters(uint32_t* p) = 0;
+  // the work the calls above queued has completed
+  virtual int sync() = 0;
+  virtual bool rccl() const = 0;
+};
+
 struct oo_gpu_rx_group {
   std::vector<oo_gpu_rx_ctx*> m;  // local members
   std::vector<int32_t> dev;       // their devices
   // join shape
   uint32_t rank = 0, nranks = 1;
-  ncclComm_t comm = nullptr;
+  Xport* x = nullptr;             // the collectives (RCCL or a caller transport)
   std::vector<GroupOp> ops;       // rank 0's changes since the last share_ops
   bool ops_lost = false;          // a change rank 0 applied but could not queue
-  void* d_ops = nullptr;          // device staging for the op broadcast: header + one chunk
   std::vector<GroupOp> h_ops;     // host staging for one chunk
-  void* d_img = nullptr;          // device staging for the table image
+  void* img = nullptr;            // staging for the table image (device, or host)
+  bool img_host = false;
   uint64_t img_bytes = 0;
 };
 
@@ -141,11 +164,11 @@ int apply_op(oo_gpu_rx_ctx* c, const GroupOp& o) {
 // replicas agree, and a member that does not is reported as -EIO.
 int group_change(oo_gpu_rx_group* g, GroupOp o) {
   if (g->m.empty()) return -EINVAL;
-  if (g->comm != nullptr && g->rank != 0) return -EPERM;  // rank 0 owns the tables
+  if (g->x != nullptr && g->rank != 0) return -EPERM;  // rank 0 owns the tables
   const int rc = apply_op(g->m[0], o);
   for (size_t i = 1; i < g->m.size(); ++i)
     if (apply_op(g->m[i], o) != rc) return -EIO;
-  if (g->comm != nullptr) {
+  if (g->x != nullptr) {
     o.rc = rc;
     try {
       g->ops.push_back(o);
@@ -174,15 +197,122 @@ GroupOp tuple_change(uint8_t kind, int af, const void* laddr, uint16_t lport, co
   return o;
 }
 
-void group_free(oo_gpu_rx_group* g) {
-  for (oo_gpu_rx_ctx* c : g->m) oo_gpu_rx_close(c);
-  if (g->d_ops) (void)hipFree(g->d_ops);
-  if (g->d_img) (void)hipFree(g->d_img);
-  if (g->comm) {
-    Rccl* r = rccl();
-    if (r) (void)r->destroy(g->comm);
+// RCCL over xGMI: host words staged through device memory allocated at the
+// join (no collective call allocates, so none fails between two
+// collectives the other ranks enter), the data buffers used in place.
+struct RcclXport final : Xport {
+  Rccl* r = nullptr;
+  ncclComm_t comm = nullptr;
+  uint32_t rank = 0, nranks = 1;
+  hipStream_t s = nullptr;  // the current call's stream
+  void* d_words = nullptr;  // kOpsHdr + one chunk of ops
+
+  ~RcclXport() override {
+    if (d_words) (void)hipFree(d_words);
+    if (comm) (void)r->destroy(comm);
   }
+  int bcast_words(void* h, uint64_t bytes) override {
+    int err = 0;
+    if (rank == 0 && hipMemcpyAsync(d_words, h, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+      err = -EIO;
+    if (r->bcast(d_words, d_words, bytes, ncclUint8, 0, comm, s) != ncclSuccess) err = -EIO;
+    if (hipMemcpyAsync(h, d_words, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      err = -EIO;
+    return err;
+  }
+  int max_words(uint32_t* h, uint32_t n) override {
+    int err = 0;
+    if (hipMemcpyAsync(d_words, h, 4ull * n, hipMemcpyHostToDevice, s) != hipSuccess) err = -EIO;
+    if (r->allreduce(d_words, d_words, n, ncclUint32, ncclMax, comm, s) != ncclSuccess) err = -EIO;
+    if (hipMemcpyAsync(h, d_words, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      err = -EIO;
+    return err;
+  }
+  int bcast_image(void* p, uint64_t bytes) override {
+    return r->bcast(p, p, bytes, ncclUint8, 0, comm, s) == ncclSuccess ? 0 : -EIO;
+  }
+  int gather(const void* src, uint64_t bytes, void* dst, const uint64_t* bytes_of) override {
+    if (r->group_start() != ncclSuccess) return -EIO;
+    ncclResult_t e = ncclSuccess;
+    if (rank == 0) {
+      uint64_t at = 0;
+      for (uint32_t k = 0; k < nranks; ++k) {
+        const uint64_t b = bytes_of[k];
+        if (k == 0 && nranks > 1) {
+          // rank 0's own records: a copy on the stream
+          if (b && dst != src &&
+              hipMemcpyAsync(dst, src, b, hipMemcpyDefault, s) != hipSuccess)
+            e = ncclSystemError;
+        } else if (b) {
+          // the other ranks' (and, in a group of one, rank 0's own through a
+          // send to itself)
+          const ncclResult_t er =
+              r->recv(static_cast<uint8_t*>(dst) + at, b, ncclUint8, (int)k, comm, s);
+          if (e == ncclSuccess) e = er;
+        }
+        at += b;
+      }
+    }
+    if ((rank != 0 || nranks == 1) && bytes > 0) {
+      const ncclResult_t er = r->send(src, bytes, ncclUint8, 0, comm, s);
+      if (e == ncclSuccess) e = er;
+    }
+    const ncclResult_t e2 = r->group_end();
+    return (e == ncclSuccess && e2 == ncclSuccess) ? 0 : -EIO;
+  }
+  int sum_counters(uint32_t* p) override {
+    return r->allreduce(p, p, OO_RX_R_COUNT, ncclUint32, ncclSum, comm, s) == ncclSuccess ? 0 : -EIO;
+  }
+  int sync() override { return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO; }
+  bool rccl() const override { return true; }
+};
+
+// A caller's transport (oo_gpu_rx_group_transport) on host memory.
+struct HostXport final : Xport {
+  oo_gpu_rx_group_transport t;
+  int bcast_words(void* h, uint64_t bytes) override { return t.bcast(t.arg, h, bytes); }
+  int max_words(uint32_t* h, uint32_t n) override { return t.max_u32(t.arg, h, n); }
+  int bcast_image(void* p, uint64_t bytes) override { return t.bcast(t.arg, p, bytes); }
+  int gather(const void* src, uint64_t bytes, void* dst, const uint64_t* bytes_of) override {
+    return t.gather(t.arg, src, bytes, dst, bytes_of);
+  }
+  int sum_counters(uint32_t* p) override { return t.sum_u32(t.arg, p, OO_RX_R_COUNT); }
+  int sync() override { return 0; }
+  bool rccl() const override { return false; }
+};
+
+void group_free(oo_gpu_rx_group* g) {
+  for (oo_gpu_rx_ctx* c : g->m) (void)oo_gpu_rx_close(c);
+  if (g->img) {
+    if (g->img_host) free(g->img);
+    else (void)hipFree(g->img);
+  }
+  delete g->x;
   delete g;
+}
+
+// Every rank learns whether any rank failed (a local error as a flag): the
+// one word all ranks decide on before a collective that only some would
+// otherwise enter.  1: some rank failed; 0: none; < 0: the agreement itself
+// failed here (the communicator is unusable; the caller abandons the group).
+int agree(oo_gpu_rx_group* g, int local_err) {
+  uint32_t w = local_err != 0 ? 1u : 0u;
+  const int e = g->x->max_words(&w, 1);
+  return e != 0 ? e : (int)w;
+}
+
+// The join-shape checks shared by the collectives: one local member and a
+// communicator or transport (a group opened in one process has neither).
+int join_shape(oo_gpu_rx_group* g, void* stream) {
+  if (g == nullptr || g->m.size() != 1) return -EINVAL;
+  if (g->x == nullptr) return g->nranks == 1 ? 1 : -ENOSYS;
+  if (g->x->rccl()) {
+    if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
+    static_cast<RcclXport*>(g->x)->s = static_cast<hipStream_t>(stream);
+  }
+  return 0;
 }
 
 }  // namespace
@@ -244,6 +374,15 @@ int oo_gpu_rx_group_join(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32
   // communicator exists: the collective calls allocate nothing, so a rank
   // never leaves one of them early on a local allocation failure.
   g->img_bytes = oo_gpu_rx_table_image_bytes(g->m[0]);
+  RcclXport* x = new (std::nothrow) RcclXport();
+  if (x == nullptr) {
+    group_free(g);
+    return -ENOMEM;
+  }
+  g->x = x;
+  x->r = r;
+  x->rank = rank;
+  x->nranks = nranks;
   try {
     g->h_ops.resize(kOpsPerChunk);
   } catch (...) {
@@ -254,15 +393,15 @@ int oo_gpu_rx_group_join(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32
     group_free(g);
     return -ENODEV;
   }
-  if (hipMalloc(&g->d_ops, kOpsHdr + sizeof(GroupOp) * kOpsPerChunk) != hipSuccess ||
-      hipMalloc(&g->d_img, g->img_bytes) != hipSuccess) {
+  if (hipMalloc(&x->d_words, kOpsHdr + sizeof(GroupOp) * kOpsPerChunk) != hipSuccess ||
+      hipMalloc(&g->img, g->img_bytes) != hipSuccess) {
     group_free(g);
     return -ENOMEM;
   }
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
-  if (r->init_rank(&g->comm, (int)nranks, u, (int)rank) != ncclSuccess) {
-    g->comm = nullptr;
+  if (r->init_rank(&x->comm, (int)nranks, u, (int)rank) != ncclSuccess) {
+    x->comm = nullptr;
     group_free(g);
     return -EIO;
   }
@@ -270,8 +409,50 @@ int oo_gpu_rx_group_join(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32
   return 0;
 }
 
-void oo_gpu_rx_group_close(oo_gpu_rx_group* g) {
-  if (g) group_free(g);
+int oo_gpu_rx_group_join_transport(oo_gpu_rx_group** out, const oo_gpu_rx_cfg* cfg, uint32_t rank,
+                                   uint32_t nranks, const oo_gpu_rx_group_transport* t) {
+  if (out == nullptr || cfg == nullptr || t == nullptr || nranks == 0 || rank >= nranks ||
+      cfg->device >= 0 || t->bcast == nullptr || t->max_u32 == nullptr || t->sum_u32 == nullptr ||
+      t->gather == nullptr)
+    return -EINVAL;
+  *out = nullptr;
+  oo_gpu_rx_group* g = nullptr;
+  int rc = oo_gpu_rx_group_open(&g, cfg, &cfg->device, 1);
+  if (rc != 0) return rc;
+  g->rank = rank;
+  g->nranks = nranks;
+  g->img_bytes = oo_gpu_rx_table_image_bytes(g->m[0]);
+  HostXport* x = new (std::nothrow) HostXport();
+  if (x == nullptr) {
+    group_free(g);
+    return -ENOMEM;
+  }
+  x->t = *t;
+  g->x = x;
+  g->img_host = true;
+  g->img = malloc(g->img_bytes);
+  try {
+    g->h_ops.resize(kOpsPerChunk);
+  } catch (...) {
+    group_free(g);
+    return -ENOMEM;
+  }
+  if (g->img == nullptr) {
+    group_free(g);
+    return -ENOMEM;
+  }
+  *out = g;
+  return 0;
+}
+
+int oo_gpu_rx_group_close(oo_gpu_rx_group* g) {
+  if (g == nullptr) return 0;
+  // (nothing is closed while a member holds registered host memory: see
+  // oo_gpu_rx_close)
+  for (oo_gpu_rx_ctx* c : g->m)
+    if (oo_gpu_rx_host_registered(c) > 0) return -EBUSY;
+  group_free(g);
+  return 0;
 }
 
 uint32_t oo_gpu_rx_group_size(const oo_gpu_rx_group* g) { return g ? (uint32_t)g->m.size() : 0; }
@@ -363,30 +544,34 @@ int oo_gpu_rx_group_gather(oo_gpu_rx_group* g, const oo_gpu_rx_shard* shards,
 }
 
 // The join shape's collectives.  Every rank enters every collective of a
-// call -- their number depends only on values all ranks share -- and a
-// local failure is reported after the last of them, never by leaving early.
-// A group opened in one process has no communicator: there they do nothing
-// (one member is its own rank 0).  A joined group of one rank runs the same
-// RCCL calls as a larger one (broadcasts and all-reduce of one rank, the
-// gather as a send/receive pair to itself).
+// call: their number depends only on values every rank holds -- broadcast
+// from rank 0, or agreed on by a one-word maximum (agree) before any rank
+// could decide alone to stop -- and a local failure after the last of them
+// is reported by the return code, never by leaving early.  A group opened in
+// one process has no communicator: there they do nothing (one member is its
+// own rank 0).  A joined group of one rank runs the same RCCL calls as a
+// larger one (broadcasts and all-reduce of one rank, the gather as a
+// send/receive pair to itself).
 
 int oo_gpu_rx_group_share_tables(oo_gpu_rx_group* g, void* stream) {
-  if (g == nullptr || g->m.size() != 1) return -EINVAL;
-  if (g->comm == nullptr) return g->nranks == 1 ? 0 : -ENOSYS;
-  Rccl* r = rccl();
-  if (r == nullptr) return -ENOSYS;
+  const int sh = join_shape(g, stream);
+  if (sh != 0) return sh > 0 ? 0 : sh;
   oo_gpu_rx_ctx* c = g->m[0];
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
   int rc = 0;
-  if (g->rank == 0) rc = oo_gpu_rx_table_export(c, g->d_img, g->img_bytes, stream);
-  // (rank 0 joins the broadcast even when its export failed: the others
-  // then import an image whose header check fails, and every rank errs)
-  if (r->bcast(g->d_img, g->d_img, g->img_bytes, ncclUint8, 0, g->comm, s) != ncclSuccess)
-    rc = rc ? rc : -EIO;
-  if (g->rank != 0) rc = oo_gpu_rx_table_import(c, g->d_img, g->img_bytes, stream);
-  if (hipStreamSynchronize(s) != hipSuccess) rc = rc ? rc : -EIO;
-  if (g->rank == 0) {
+  if (g->rank == 0) rc = oo_gpu_rx_table_export(c, g->img, g->img_bytes, stream);
+  // (rank 0 joins the broadcast even when its export failed)
+  const int e = g->x->bcast_image(g->img, g->img_bytes);
+  if (rc == 0) rc = e;
+  if (rc == 0) rc = g->x->sync();
+  // No replica imports unless every rank has the image: the staging may
+  // still hold the previous share's, which would pass the import's checks.
+  const int any = agree(g, rc);
+  if (any < 0) return any;
+  if (any) return rc ? rc : -EIO;
+  if (g->rank != 0) {
+    rc = oo_gpu_rx_table_import(c, g->img, g->img_bytes, stream);
+    if (rc == 0) rc = g->x->sync();
+  } else {
     g->ops.clear();  // rank 0's changes so far are in the image
     g->ops_lost = false;
   }
@@ -394,37 +579,26 @@ int oo_gpu_rx_group_share_tables(oo_gpu_rx_group* g, void* stream) {
 }
 
 int oo_gpu_rx_group_share_ops(oo_gpu_rx_group* g, void* stream) {
-  if (g == nullptr || g->m.size() != 1) return -EINVAL;
-  if (g->comm == nullptr) return g->nranks == 1 ? 0 : -ENOSYS;
-  Rccl* r = rccl();
-  if (r == nullptr) return -ENOSYS;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
+  const int sh = join_shape(g, stream);
+  if (sh != 0) return sh > 0 ? 0 : sh;
   int err = 0;
   auto fail = [&err](int e) {
     if (err == 0) err = e;
   };
-  // The header: the count and rank 0's flags.
+  // The header: the count and rank 0's flags.  Then every rank learns
+  // whether every rank has it before any enters the body broadcasts.
   uint64_t hdr[2] = {g->rank == 0 ? (uint64_t)g->ops.size() : 0,
                      g->rank == 0 && g->ops_lost ? kOpsLost : 0u};
-  if (g->rank == 0 && hipMemcpyAsync(g->d_ops, hdr, kOpsHdr, hipMemcpyHostToDevice, s) != hipSuccess)
-    fail(-EIO);
-  if (r->bcast(g->d_ops, g->d_ops, kOpsHdr, ncclUint8, 0, g->comm, s) != ncclSuccess) fail(-EIO);
-  if (hipMemcpyAsync(hdr, g->d_ops, kOpsHdr, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    fail(-EIO);
-  if (err != 0) return err;  // no rank has a count it can trust: none goes on
+  const int eh = g->x->bcast_words(hdr, kOpsHdr);
+  const int any = agree(g, eh);
+  if (any < 0) return any;
+  if (any) return eh ? eh : -EIO;  // some rank has no count: none goes on (rank 0 keeps its ops)
   const uint64_t cnt = hdr[0];
-  uint8_t* body = static_cast<uint8_t*>(g->d_ops) + kOpsHdr;
   for (uint64_t at = 0; at < cnt; at += kOpsPerChunk) {
     const uint64_t k = std::min<uint64_t>(kOpsPerChunk, cnt - at);
     const uint64_t bytes = sizeof(GroupOp) * k;
-    if (g->rank == 0 &&
-        hipMemcpyAsync(body, g->ops.data() + at, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-      fail(-EIO);
-    if (r->bcast(body, body, bytes, ncclUint8, 0, g->comm, s) != ncclSuccess) fail(-EIO);
-    if (hipMemcpyAsync(g->h_ops.data(), body, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
+    if (g->rank == 0) memcpy(g->h_ops.data(), g->ops.data() + at, bytes);
+    if (g->x->bcast_words(g->h_ops.data(), bytes) != 0) {
       fail(-EIO);
       continue;
     }
@@ -449,62 +623,59 @@ int oo_gpu_rx_group_share_ops(oo_gpu_rx_group* g, void* stream) {
 int oo_gpu_rx_group_gather_rccl(oo_gpu_rx_group* g, const oo_gpu_rx_result* d_out, uint32_t n,
                                 oo_gpu_rx_result* d_dst, const uint32_t* counts, void* stream) {
   if (g == nullptr || g->m.size() != 1 || (n > 0 && d_out == nullptr)) return -EINVAL;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
-  if (g->comm == nullptr) {
+  if (g->x == nullptr) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
     if (g->nranks != 1) return -ENOSYS;
+    if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
     if (d_dst != nullptr && n > 0 && d_dst != d_out &&
         hipMemcpyAsync(d_dst, d_out, sizeof(oo_gpu_rx_result) * n, hipMemcpyDefault, s) != hipSuccess)
       return -EIO;
     return 0;
   }
-  Rccl* r = rccl();
-  if (r == nullptr) return -ENOSYS;
-  // (rank 0 without a destination is a caller error the other ranks cannot
-  // see: their sends to it never complete)
-  if (g->rank == 0 && (d_dst == nullptr || counts == nullptr || counts[0] != n)) return -EINVAL;
-  if (r->group_start() != ncclSuccess) return -EIO;
-  ncclResult_t e = ncclSuccess;
-  if (g->rank == 0) {
-    uint64_t at = 0;
-    for (uint32_t k = 0; k < g->nranks; ++k) {
-      const uint64_t bytes = sizeof(oo_gpu_rx_result) * (uint64_t)counts[k];
-      if (k == 0 && g->nranks > 1) {
-        // rank 0's own records: a copy on the stream
-        if (bytes && d_dst != d_out &&
-            hipMemcpyAsync(d_dst, d_out, bytes, hipMemcpyDefault, s) != hipSuccess)
-          e = ncclSystemError;
-      } else if (bytes) {
-        // the other ranks' (and, in a group of one, rank 0's own through a
-        // send to itself)
-        const ncclResult_t er = r->recv(reinterpret_cast<uint8_t*>(d_dst) + at, bytes, ncclUint8,
-                                        (int)k, g->comm, s);
-        if (e == ncclSuccess) e = er;
-      }
-      at += bytes;
+  const int sh = join_shape(g, stream);
+  if (sh != 0) return sh;
+  // Rank 0's counts (and whether it has a destination) to every rank; each
+  // checks its own entry, and all agree before any record moves: a count
+  // that does not match its rank's n is -EINVAL on every rank, where it
+  // would otherwise hang or truncate the gather.
+  std::vector<uint32_t> w;
+  std::vector<uint64_t> bytes_of;
+  try {
+    w.assign(g->nranks + 1u, 0u);
+    bytes_of.assign(g->nranks, 0u);
+  } catch (...) {
+    w.clear();
+  }
+  int local = 0;
+  if (w.empty() || 4ull * w.size() > kOpsHdr + sizeof(GroupOp) * kOpsPerChunk) {
+    // (no words to exchange: still enter both collectives, with one word)
+    uint32_t dummy[1] = {0};
+    (void)g->x->bcast_words(dummy, 4);
+    local = 2;
+  } else {
+    if (g->rank == 0) {
+      w[0] = (d_dst != nullptr && counts != nullptr) ? 1u : 0u;
+      if (counts != nullptr)
+        for (uint32_t k = 0; k < g->nranks; ++k) w[1 + k] = counts[k];
     }
+    if (g->x->bcast_words(w.data(), 4ull * w.size()) != 0) local = 2;
+    else if (w[0] == 0 || w[1 + g->rank] != n) local = 1;
   }
-  if ((g->rank != 0 || g->nranks == 1) && n > 0) {
-    const ncclResult_t er =
-        r->send(d_out, sizeof(oo_gpu_rx_result) * (uint64_t)n, ncclUint8, 0, g->comm, s);
-    if (e == ncclSuccess) e = er;
-  }
-  const ncclResult_t e2 = r->group_end();
-  return (e == ncclSuccess && e2 == ncclSuccess) ? 0 : -EIO;
+  uint32_t v = (uint32_t)local;
+  const int ea = g->x->max_words(&v, 1);
+  if (ea != 0) return ea;
+  if (v != 0) return v == 1 ? -EINVAL : -EIO;
+  for (uint32_t k = 0; k < g->nranks; ++k) bytes_of[k] = sizeof(oo_gpu_rx_result) * (uint64_t)w[1 + k];
+  return g->x->gather(d_out, sizeof(oo_gpu_rx_result) * (uint64_t)n, d_dst, bytes_of.data());
 }
 
 int oo_gpu_rx_group_sum_counters(oo_gpu_rx_group* g, oo_gpu_rx_counters* d_counters, void* stream) {
   if (g == nullptr || g->m.size() != 1 || d_counters == nullptr) return -EINVAL;
-  if (g->comm == nullptr) return g->nranks == 1 ? 0 : -ENOSYS;
-  Rccl* r = rccl();
-  if (r == nullptr) return -ENOSYS;
-  if (hipSetDevice(g->dev[0]) != hipSuccess) return -ENODEV;
-  return r->allreduce(d_counters, d_counters, OO_RX_R_COUNT, ncclUint32, ncclSum, g->comm,
-                      static_cast<hipStream_t>(stream)) == ncclSuccess
-             ? 0
-             : -EIO;
+  const int sh = join_shape(g, stream);
+  if (sh != 0) return sh > 0 ? 0 : sh;
+  return g->x->sum_counters(d_counters->by_reason);
 }
 
-int oo_gpu_rx_group_uses_rccl(const oo_gpu_rx_group* g) { return g && g->comm ? 1 : 0; }
+int oo_gpu_rx_group_uses_rccl(const oo_gpu_rx_group* g) { return g && g->x && g->x->rccl() ? 1 : 0; }
 
 }  // extern "C"

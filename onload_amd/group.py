@@ -32,6 +32,18 @@ class Shard(ctypes.Structure):
 
 assert ctypes.sizeof(Shard) == 56
 
+# oo_gpu_rx_group_transport: a caller's collectives on host memory.
+BCAST = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+REDUCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                          ctypes.c_uint32)
+GATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [("arg", ctypes.c_void_p), ("bcast", BCAST), ("max_u32", REDUCE),
+                ("sum_u32", REDUCE), ("gather", GATHER)]
+
 
 def _check(rc: int, what: str) -> int:
     if rc < 0:
@@ -56,7 +68,15 @@ class GpuRxGroup:
                  ip6_log2: int = 14, intf_hwport=(0,), _join=None):
         self._lib = _abi.load_library()
         g = ctypes.c_void_p()
-        if _join is None:
+        if _join is not None and _join[0] == "transport":
+            _, rank, nranks, t = _join
+            cfg = _cfg(-1, max_socks, ip4_log2, ip6_log2, intf_hwport)
+            self._transport = t  # the callbacks live as long as the group
+            _check(self._lib.oo_gpu_rx_group_join_transport(ctypes.byref(g), ctypes.byref(cfg),
+                                                            rank, nranks, ctypes.byref(t)),
+                   "oo_gpu_rx_group_join_transport")
+            self.devices = [-1]
+        elif _join is None:
             devs = (ctypes.c_int32 * len(devices))(*devices)
             cfg = _cfg(0, max_socks, ip4_log2, ip6_log2, intf_hwport)
             _check(self._lib.oo_gpu_rx_group_open(ctypes.byref(g), ctypes.byref(cfg), devs,
@@ -89,6 +109,12 @@ class GpuRxGroup:
         """This process's member of a group across processes (one per GPU)."""
         return cls(_join=(device, rank, nranks, gid), **kw)
 
+    @classmethod
+    def join_transport(cls, rank: int, nranks: int, transport: Transport, **kw) -> "GpuRxGroup":
+        """This process's host-only member of a group whose collectives run
+        over the caller's transport (oo_gpu_rx_group_join_transport)."""
+        return cls(_join=("transport", rank, nranks, transport), **kw)
+
     @property
     def rank(self) -> int:
         return int(self._lib.oo_gpu_rx_group_rank(self._g))
@@ -100,9 +126,11 @@ class GpuRxGroup:
 
     def close(self) -> None:
         if self._g:
+            rc = self._lib.oo_gpu_rx_group_close(self._g)
+            if rc:  # -EBUSY: a member holds registered host memory; nothing closed
+                raise OSError(-rc, "oo_gpu_rx_group_close: unregister host memory first")
             for m in self.members:
                 m._ctx = None
-            self._lib.oo_gpu_rx_group_close(self._g)
             self._g = None
 
     def __del__(self):

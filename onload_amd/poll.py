@@ -131,6 +131,7 @@ class RxPoll:
                  crossover: dict | None = None):
         self._lib = load_poll()
         self.pool = pool
+        self.stack = stack  # the shim's context outlives it (its registrations are the shim's)
         self.h = handlers
         h = handlers
         fut = lambda a, i, f, r, fu: int(h.post_future(  # noqa: E731

@@ -23,6 +23,7 @@ from __future__ import annotations
 import ctypes
 import errno
 import ipaddress
+import mmap
 from typing import Optional, Union
 
 import numpy as np
@@ -30,6 +31,7 @@ import numpy as np
 from . import _abi
 
 Addr = Union[bytes, str, None]
+PAGE = mmap.PAGESIZE
 
 
 def htons(port: int) -> int:
@@ -107,7 +109,9 @@ class GpuRxStack:
             self._ctx = None
             return
         if self._ctx:
-            self._lib.oo_gpu_rx_close(self._ctx)
+            rc = self._lib.oo_gpu_rx_close(self._ctx)
+            if rc:  # -EBUSY: host memory still registered; the context stays open
+                raise OSError(-rc, "oo_gpu_rx_close: unregister host memory first")
             self._ctx = None
 
     def __enter__(self):
@@ -312,12 +316,17 @@ class GpuRxStack:
         return img
 
     # -- host memory the device reads directly --------------------------
-    def host_register(self, arr: np.ndarray) -> int:
-        """hipHostRegister (mapped) the array's memory; returns its device
-        address."""
+    def host_register(self, arr: np.ndarray, nbytes: Optional[int] = None) -> int:
+        """oo_gpu_rx_host_register: hipHostRegister (mapped) the whole pages
+        holding the array -- from its first byte, which must start a page,
+        through the page holding its last (nbytes: that many bytes instead,
+        a multiple of the page size).  Those pages must be the caller's own
+        (tests/hostmem.page_buffer); returns the device address."""
+        if nbytes is None:
+            nbytes = -(-arr.nbytes // PAGE) * PAGE
         d = ctypes.c_void_p()
         rc = self._lib.oo_gpu_rx_host_register(self._ctx, ctypes.c_void_p(arr.ctypes.data),
-                                               arr.nbytes, ctypes.byref(d))
+                                               nbytes, ctypes.byref(d))
         if rc:
             raise OSError(-rc, "oo_gpu_rx_host_register")
         return int(d.value or 0)
@@ -326,6 +335,10 @@ class GpuRxStack:
         rc = self._lib.oo_gpu_rx_host_unregister(self._ctx, ctypes.c_void_p(arr.ctypes.data))
         if rc:
             raise OSError(-rc, "oo_gpu_rx_host_unregister")
+
+    def host_registered(self) -> int:
+        """oo_gpu_rx_host_registered: ranges the context holds."""
+        return int(self._lib.oo_gpu_rx_host_registered(self._ctx))
 
     # -- asynchronous host-memory batches -------------------------------
     def submit(self, frames: np.ndarray, desc: np.ndarray, out: np.ndarray,

@@ -85,10 +85,11 @@ static void free_pages(void* p, uint64_t bytes)
     munmap(p, page_bytes(bytes));
 }
 
-/* Registers p with the device; 1 and *d set on success. */
+/* Registers the whole pages of one of the shim's own buffers (alloc_pages)
+ * with the device; 1 and *d set on success. */
 static int reg(oo_gpu_rx_ctx* gpu, void* p, uint64_t bytes, void** d)
 {
-  return oo_gpu_rx_host_register(gpu, p, bytes, d) == 0;
+  return oo_gpu_rx_host_register(gpu, p, page_bytes(bytes), d) == 0;
 }
 
 static void chunk_free(oo_rx_poll* p, struct chunk* c)
@@ -162,8 +163,8 @@ int oo_rx_poll_open(oo_rx_poll** out, oo_gpu_rx_ctx* gpu, const oo_rx_poll_cfg* 
   /* Zero copy: the kernel reads each frame where the NIC put it.  If the
    * pool cannot be registered the shim gathers instead. */
   if( (cfg->flags & OO_RX_POLL_ZERO_COPY) && cfg->pkt_bufs_bytes > 0 &&
-      reg(gpu, (void*)cfg->pkt_bufs, cfg->pkt_bufs_bytes, &p->d_pool) )
-    p->zero_copy = 1;
+      oo_gpu_rx_host_register(gpu, (void*)cfg->pkt_bufs, cfg->pkt_bufs_bytes, &p->d_pool) == 0 )
+    p->zero_copy = 1;  /* (a pool that is not whole pages: -EINVAL, gathered) */
   /* A transformed frame lies inside its buffer (frame_of): a gather buffer
    * of evs_per_poll 64-B-aligned buffers holds any chunk. */
   p->pack_bytes = (uint64_t)n * up64(cfg->buf_size);

@@ -13,6 +13,11 @@ PAGE = mmap.PAGESIZE
 _KEEP = []
 
 
+def whole_pages(nbytes: int) -> int:
+    """nbytes rounded up to whole pages (a registration's size)."""
+    return -(-int(nbytes) // PAGE) * PAGE
+
+
 def page_buffer(count: int, dtype=np.uint8) -> np.ndarray:
     """A zeroed array of `count` items on pages of its own."""
     nbytes = max(1, int(count) * np.dtype(dtype).itemsize)

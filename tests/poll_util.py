@@ -21,7 +21,7 @@ from collections import Counter
 
 import numpy as np
 
-from hostmem import page_buffer
+from hostmem import page_buffer, whole_pages
 from onload_amd import _abi, poll
 
 CSUM_CLASS = poll.DISCARD_L3_CSUM_ERR | poll.DISCARD_L4_CSUM_ERR | poll.DISCARD_L3_CLASS_OTHER
@@ -193,7 +193,7 @@ def events_for(frames, buf_size, rng, discard_mix=True):
     whole-buffer RX events; with discard_mix, also discard events of every
     class, multi-buffer events and events pointing outside the pool."""
     n = len(frames)
-    pool = page_buffer((n + 1) * buf_size)
+    pool = page_buffer(whole_pages((n + 1) * buf_size))  # whole pages: registrable
     evs = np.zeros(n, dtype=poll.EV_DTYPE)
     for i, (f, intf) in enumerate(frames):
         ofs = int(rng.choice([192, 192, 193, 256, 0, 255]))

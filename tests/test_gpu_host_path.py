@@ -244,3 +244,74 @@ def test_xdp_frames_and_ring_flush_with_registered_page_ends(cuda):
     g.host_unregister(ring)
     g.host_unregister(umem)
     g.close()
+
+
+def _libc():
+    import ctypes
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                          ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    return libc
+
+
+def test_register_unregister_unmap_then_pageable_copies_at_the_same_address(cuda):
+    """The round-5 faults' lifetime, the legal way round (DESIGN.md §5 round
+    6): pages registered with a context and read in place by a batch, then
+    unregistered, unmapped, and mapped again at the same address as ordinary
+    pageable memory; torch's pageable copies to and from that address (the
+    copies the faults were reported at) move the new bytes, both a copy
+    large enough for the runtime to pin it in place and a small one.  The
+    context closes only once nothing is registered."""
+    import ctypes
+    torch = cuda
+    libc = _libc()
+    PROT_RW, MAP_PRIV_ANON, MAP_FIXED_NOREPLACE = 0x3, 0x22, 0x100000
+    filters, socks = pktgen.world(2)
+    n = 4096
+    buf0, desc = pktgen.generate(2, n, first=777)
+    size = -(-buf0.nbytes // PAGE) * PAGE + (64 << 20)  # the batch's frames, then 64 MiB more
+    addr = libc.mmap(None, size, PROT_RW, MAP_PRIV_ANON, -1, 0)
+    assert addr not in (None, ctypes.c_void_p(-1).value)
+    host = np.frombuffer((ctypes.c_uint8 * size).from_address(addr), np.uint8)
+    host[:buf0.nbytes] = buf0
+    g = GpuRxStack(device=0, host_stage_bytes=1 << 20, host_stage_pkts=n)
+    g.load_world(filters, socks)
+    o = OracleStack()
+    o.load_world(filters, socks)
+    d = g.host_register(host, nbytes=size)
+    assert d != 0 and g.host_registered() == 1
+    # the frames read in place by the kernel: the mapping is used
+    dd = torch.from_numpy(desc.view(np.uint8).copy()).to("cuda")
+    out = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    g.handle_rx_batch_dev(d, buf0.nbytes, dd.data_ptr(), n, out.data_ptr(), 0, s.cuda_stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(_abi.RESULT_DTYPE)
+    want = o.handle_rx_batch(buf0, desc, nthreads=8)
+    assert got.tobytes() == want.tobytes(), diff_report(got, want, desc)
+    with pytest.raises(OSError) as e:  # still registered: the context stays open
+        g.close()
+    assert e.value.errno == errno.EBUSY
+    g.host_unregister(host)
+    del host
+    assert libc.munmap(ctypes.c_void_p(addr), size) == 0
+    again = libc.mmap(ctypes.c_void_p(addr), size, PROT_RW, MAP_PRIV_ANON | MAP_FIXED_NOREPLACE,
+                      -1, 0)
+    assert again == addr, "the kernel did not give the same address back"
+    fresh = np.frombuffer((ctypes.c_uint8 * size).from_address(addr), np.uint8)
+    rng = np.random.default_rng(3)
+    for nbytes in (size, 4096 * 3 + 100):
+        src = rng.integers(0, 256, nbytes, dtype=np.uint8)
+        fresh[:nbytes] = src
+        dev = torch.from_numpy(fresh[:nbytes]).to("cuda")  # pageable H2D from those pages
+        torch.cuda.synchronize()
+        assert torch.equal(dev.cpu(), torch.from_numpy(src))
+        dev.add_(1)
+        torch.from_numpy(fresh[:nbytes]).copy_(dev)  # pageable D2H into those pages
+        torch.cuda.synchronize()
+        assert (fresh[:nbytes] == (src + 1).astype(np.uint8)).all()
+    del fresh
+    assert libc.munmap(ctypes.c_void_p(addr), size) == 0
+    g.close()

@@ -25,6 +25,7 @@
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <sys/mman.h>
 #include <string.h>
 #include <time.h>
 
@@ -106,10 +107,11 @@ int main(int argc, char** argv)
     return 3;
   /* The AF_XDP layout: frame i in buffer i at HEADROOM (single-buffer frames
    * only: the shim hands a frame that overruns its buffer back). */
-  pool_bytes = (uint64_t)n * BUF;
-  if( posix_memalign((void**)&pool, 4096, pool_bytes) )
+  /* (whole pages of its own, as oo_gpu_rx_host_register requires) */
+  pool_bytes = ((uint64_t)n * BUF + 4095) & ~(uint64_t)4095;
+  pool = mmap(NULL, pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if( pool == MAP_FAILED )
     return 3;
-  memset(pool, 0, pool_bytes);
   evs = calloc(n, sizeof(*evs));
   for( i = 0; i < n; ++i ) {
     uint32_t len = desc[i].len;
@@ -218,6 +220,7 @@ int main(int argc, char** argv)
     }
   }
   oo_gpu_rx_close(gpu);
+  munmap(pool, pool_bytes);
   oo_or_tables_free(ot);
   return 0;
 }
