@@ -75,7 +75,7 @@ check-integration: oracle
 	  -I$(REF)/src/lib/transport/common -I$(REF)/src/lib/ciul -I$(REF)/src/lib/citools \
 	  -Iinclude -o build/netif_event_gpu.o integration/netif_event_gpu.c
 
-.PHONY: all oracle asm clean variants poll-variants check-integration
+.PHONY: all oracle asm clean variants check-integration
 
 tools/poll_rtt: tools/poll_rtt.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
@@ -93,11 +93,3 @@ tools/poll_bench: tools/poll_bench.c $(SHIM) $(PKTGEN) oracle include/oo_rx_poll
 	  -l:liboo_gpu_rx.so -l:liboo_pktgen.so -Loracle -l:liboorx_oracle.so \
 	  -Wl,-rpath,'$$ORIGIN/../onload_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
-# Builds for tools/poll_ab.sh (build/pollvar/<name>/liboo_gpu_rx.so); not part
-# of `all`.
-POLL_VARIANTS ?= pollres:-DOO_POLL_MAX=256,-DOO_RES_MAX=256 \
-                  pollresinl:-DOO_POLL_MAX=256,-DOO_RES_MAX=256,-DOO_POLL_INLINE=128 \
-                  doneev:-DOO_DONE_EVENT=1
-poll-variants: $(SRCS) $(HDRS)
-	for v in $(POLL_VARIANTS); do n=$${v%%:*}; f=$$(echo "$${v#*:}" | tr ',' ' '); mkdir -p build/pollvar/$$n; \
-	  $(HIPCC) $(HIPFLAGS) $$f -shared -Wl,-soname,liboo_gpu_rx.so -o build/pollvar/$$n/liboo_gpu_rx.so $(SRCS) -ldl || exit 1; done

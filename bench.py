@@ -474,7 +474,7 @@ def run_rank(args) -> None:
 PATH_KERNELS = {1: ["oo_rx::rx_kernel"], 2: ["oo_rx_short::rx_kernel"],
                 3: ["oo_rx::win_kernel", "oo_rx::body_kernel"],
                 4: ["oo_rx::win_kernel", "oo_rx_short::body_kernel"],
-                5: ["oo_rx_poll::rx_kernel"], 6: ["oo_rx_poll::rx_resident"]}
+                5: ["oo_rx_poll::rx_kernel"]}
 
 
 def time_scatter(torch, dist, shards, cfg, seed, n_total, rank, world, dev, my_buf,

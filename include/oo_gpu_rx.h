@@ -238,11 +238,10 @@ uint64_t oo_gpu_rx_table_gen(const oo_gpu_rx_ctx* ctx);
 /* Which kernels transformed the context's last batch: 1 rx_kernel with the
  * 4-slot ring, 2 its 2-slot instance, 3 the split transform (win_kernel +
  * body_kernel with lockstep slots), 4 the split transform with the
- * per-group-sequence body_kernel, 5 the poll instance (12-slot ring; only
- * in a library built with OO_POLL_MAX=256: path 4, and batches of at most
- * 256 packets), 6 the resident poll kernel (the same tile loop, no launch; in
- * a library built with OO_RES_MAX=256); 0 none yet.  For measurements: which
- * kernels a timed launch's duration covers. */
+ * per-group-sequence body_kernel, 5 the poll instance (12-slot ring, 8-packet
+ * tiles: batches of at most 256 packets; a submit_mapped batch's completion
+ * written by the kernel); 0 none yet.  For measurements: which kernels a
+ * timed launch's duration covers. */
 uint32_t oo_gpu_rx_last_path(const oo_gpu_rx_ctx* ctx);
 /* Table maintenance so far: flushes of queued changes to the device, and how
  * the key index followed each -- rebuilt from the tables, or updated for the
@@ -257,23 +256,6 @@ typedef struct oo_gpu_rx_table_stats {
   uint32_t rsvd;
 } oo_gpu_rx_table_stats;
 int oo_gpu_rx_get_table_stats(oo_gpu_rx_ctx* ctx, oo_gpu_rx_table_stats* out);
-/* The resident poll kernel (only in a library built with
- * OO_POLL_MAX=256 OO_RES_MAX=256, not the product build): a context that submits
- * oo_gpu_rx_submit_mapped batches of at most 256 packets starts a small
- * grid that stays on the device and takes them from a doorbell in host
- * memory, with no launch per batch; it leaves after 200 ms without one (and
- * when the context closes).  Until it runs, and whenever it may have left,
- * batches take the launch path.  Counts so far: batches it took, of them
- * re-run through a launch (it had left before taking them), instances
- * started; running: one was seen polling and was rung within its window.
- * For tests and measurements. */
-typedef struct oo_gpu_rx_resident_stats {
-  uint64_t batches;
-  uint64_t fallbacks;
-  uint32_t instances;
-  uint32_t running;
-} oo_gpu_rx_resident_stats;
-int oo_gpu_rx_get_resident_stats(const oo_gpu_rx_ctx* ctx, oo_gpu_rx_resident_stats* out);
 /* Streams.  The context remembers the streams it launched on (nothing is
  * recorded per batch): a table change enqueues an event on each of them at
  * that moment and waits for it, so every stream used with the context must
@@ -326,8 +308,7 @@ typedef struct oo_gpu_rx_tuning {
                               2 the same with the 2-slot ring; 3 the split
                               transform (win_kernel + body_kernel); 4 the
                               poll instance (12-slot ring; a submit_mapped
-                              batch's completion written by the kernel) in
-                              a library built with it, else as 1           */
+                              batch's completion written by the kernel)    */
   uint32_t grid_pct;       /* % of the resident grid to launch (0: 100)       */
   uint32_t groups;         /* tile-claim groups at most (0: by frame size)    */
   int32_t  gshift;         /* a group's wave runs, log2 (-1: by frame size)   */

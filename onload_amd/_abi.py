@@ -116,12 +116,6 @@ class TableStats(ctypes.Structure):
                 ("rsvd", ctypes.c_uint32)]
 
 
-class ResidentStats(ctypes.Structure):
-    """oo_gpu_rx_resident_stats."""
-    _fields_ = [("batches", ctypes.c_uint64), ("fallbacks", ctypes.c_uint64),
-                ("instances", ctypes.c_uint32), ("running", ctypes.c_uint32)]
-
-
 class IoVec(ctypes.Structure):
     _fields_ = [("iov_base", ctypes.c_void_p), ("iov_len", ctypes.c_size_t)]
 
@@ -171,7 +165,6 @@ ABI_SYMBOLS = {
     "oo_gpu_rx_table_gen": (ctypes.c_uint64, [_P]),
     "oo_gpu_rx_last_path": (ctypes.c_uint32, [_P]),
     "oo_gpu_rx_get_table_stats": (ctypes.c_int, [_P, _P]),
-    "oo_gpu_rx_get_resident_stats": (ctypes.c_int, [_P, _P]),
     "oo_gpu_rx_set_len_hint": (ctypes.c_int, [_P, _U32]),
     "oo_gpu_rx_set_tuning": (ctypes.c_int, [_P, ctypes.POINTER(Tuning)]),
     "oo_gpu_rx_process_dev": (ctypes.c_int, [_P, _P, _U64, _P, _U32, _P, _P, _P]),

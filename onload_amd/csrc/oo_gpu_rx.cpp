@@ -45,7 +45,6 @@ extern "C" int oo_rx_blocks_per_cu_short(void);
 extern "C" int oo_rx_waves_per_block(void);
 extern "C" int oo_rx_launch_poll(const oo_rx::PollArgs* A, int grid, hipStream_t stream);
 extern "C" int oo_rx_blocks_per_cu_poll(void);
-extern "C" int oo_rx_launch_resident(const oo_rx::ResArgs* A, int grid, hipStream_t stream);
 extern "C" int oo_rx_win_blocks_per_cu(void);
 extern "C" int oo_rx_body_blocks_per_cu(void);
 extern "C" int oo_rx_win_waves_per_block(void);
@@ -127,38 +126,13 @@ static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
 #endif
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
 constexpr uint32_t SMALL_N = 2048;    // launch(): batches up to this many packets take 8-packet tiles
-// The poll instance (auto) up to OO_POLL_MAX packets, writing a
-// submit_mapped batch's done word itself up to OO_POLL_DONE_MAX (build-time
-// knobs for same-box A/Bs: tools/poll_ab.sh).  Not in the product build
-// (OO_POLL_INSTANCE 0: no launch of it at all, the tuning path 4 runs
-// rx_kernel): every process in which the GPU faulted this round had run it,
-// none before it went in; the cause is not found.
-// Built with OO_POLL_MAX=256 OO_RES_MAX=256 (make poll-variants: pollres) it
-// takes a poll's batches, and the resident kernel those of
-// oo_gpu_rx_submit_mapped.
-// The resident poll kernel (oo_rx_kernel.hip "The resident poll kernel")
-// takes submit_mapped batches of at most OO_RES_MAX packets (0: never) once
-// it runs; OO_RES_WAVES waves, a tile of eight packets each.
-#ifndef OO_RES_MAX
-#define OO_RES_MAX 0  // not in the product build: see OO_POLL_MAX below
-#endif
-constexpr uint32_t RES_WAVES = 32;
-static_assert(OO_RES_MAX <= 8 * RES_WAVES, "a resident batch is one 8-packet tile per wave at most");
-// It leaves after 200 ms without a batch; the host rings it only within
-// 100 ms of its last ring (or of seeing it start), else starts a new one.
-constexpr uint64_t kResIdleTicks = 20000000ull;  // s_memrealtime, 100 MHz
-constexpr int64_t kResUsableNs = 100 * 1000 * 1000;
+// The poll instance (auto) up to OO_POLL_MAX packets -- a poll's batch:
+// tools/poll_bench, DESIGN.md §5e -- writing a submit_mapped batch's done
+// word itself up to OO_POLL_DONE_MAX (0: the instance never runs).
 #ifndef OO_POLL_MAX
-#define OO_POLL_MAX 0
+#define OO_POLL_MAX 256
 #endif
-#ifndef OO_POLL_INSTANCE
-#define OO_POLL_INSTANCE (OO_POLL_MAX > 0 || OO_RES_MAX > 0)
-#endif
-#ifndef OO_DONE_EVENT
-// 1: a host-path batch completes by its event alone (the waiter spins on
-// hipEventQuery) -- no stream-written done word (A/B knob, make poll-variants).
-#define OO_DONE_EVENT 0
-#endif
+#define OO_POLL_INSTANCE (OO_POLL_MAX > 0)
 #ifndef OO_POLL_DONE_MAX
 #define OO_POLL_DONE_MAX 2048
 #endif
@@ -219,13 +193,6 @@ struct HostSlot {
   uint32_t* h_done = nullptr;  // pinned: the slot's last completed ticket (low 32 bits),
   uint32_t* d_done = nullptr;  //   written by the stream after the batch (complete_slot spins on it)
   bool busy = false;
-  // A batch rung to the resident kernel: what re-running it needs (the
-  // launch path, if the resident instance left without taking it).
-  bool res = false;
-  const void* r_frames = nullptr;
-  uint64_t r_frames_bytes = 0;
-  const oo_gpu_pkt_desc* r_desc = nullptr;
-  oo_gpu_rx_result* r_out = nullptr;
   uint64_t ticket = 0;
   uint32_t n = 0;
   oo_gpu_rx_result* out = nullptr;  // caller's buffer
@@ -308,28 +275,11 @@ struct oo_gpu_rx_ctx {
   uint32_t grid_short = 0;     // resident blocks of the short-frame rx_kernel (0: unused)
   uint32_t grid_poll = 0;      // resident blocks of the poll instance's rx_kernel (0: unused)
   // A submit_mapped batch's completion, handed to launch(): the slot's done
-  // word and value, and the batch's descriptors in host memory (null: not
-  // known); launch() sets done_by_kernel when the poll instance writes it.
+  // word and value; launch() sets done_by_kernel when the poll instance
+  // writes it.
   uint32_t* poll_done = nullptr;
   uint32_t poll_done_val = 0;
-  const oo_gpu_pkt_desc* poll_h_desc = nullptr;
   bool done_by_kernel = false;
-  // The resident poll kernel: its stream, mailboxes and doorbell / alive
-  // words (host memory, device-mapped), the per-batch counters (device),
-  // the last batch number rung, the instance epoch launched and whether it
-  // was seen polling, the host time of its last ring (or start seen), the
-  // table generation of its last batch.
-  hipStream_t res_s = nullptr;
-  oo_rx::ResMail* h_mail = nullptr;
-  oo_rx::ResMail* d_mail = nullptr;
-  uint32_t* h_bell = nullptr;  // [0] doorbell, [32] alive
-  uint32_t* d_bell = nullptr;
-  uint32_t* d_res_ctr = nullptr;
-  uint32_t res_seq = 0, res_epoch = 0;
-  bool res_launched = false, res_seen = false;
-  int64_t res_last_ns = 0;
-  uint64_t res_tables_gen = ~0ull;
-  uint64_t n_res = 0, n_res_fallback = 0;
   std::vector<void*> retired;  // replaced pending-word buffers (freed at close)
   uint32_t ncu = 0, bpc[6] = {0, 0, 0, 0, 0, 0};  // CUs; resident blocks per CU of the six kernels
   uint32_t grid_win = 0;       // resident blocks of win_kernel (split transform)
@@ -365,12 +315,8 @@ struct oo_gpu_rx_ctx {
   uint8_t* h_image_hdr = nullptr;  // pinned 64-B table image header
 };
 
-// Every batch rung to the resident poll kernel has completed; a slot's
-// done word seen by spinning; a rung batch re-run (below).
-static int res_quiesce(oo_gpu_rx_ctx* c);
-static int64_t now_ns();
+// A slot's done word seen by spinning (below).
 static bool spin_done(const HostSlot& s);
-static int res_recover(oo_gpu_rx_ctx* c, HostSlot& s);
 
 namespace {
 
@@ -709,10 +655,6 @@ void free_dev(oo_gpu_rx_ctx* c) {
   }
   for (void* p : c->retired) (void)hipFree(p);
   if (c->tables_ev) (void)hipEventDestroy(c->tables_ev);
-  if (c->res_s) (void)hipStreamDestroy(c->res_s);
-  if (c->h_mail) (void)hipHostFree(c->h_mail);
-  if (c->h_bell) (void)hipHostFree(c->h_bell);
-  if (c->d_res_ctr) (void)hipFree(c->d_res_ctr);
   if (c->h_image_hdr) (void)hipHostFree(c->h_image_hdr);
   if (c->h_kx_req) (void)hipHostFree(c->h_kx_req);
   if (c->h_len) (void)hipHostFree(c->h_len);
@@ -811,7 +753,7 @@ void mark_kx_owners(TableOp* h, uint32_t n) {
 // than apply the queued ops twice.
 int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
   if (c->ops.empty()) return 0;
-  if (order_after_batches(c, s) != 0 || res_quiesce(c) != 0) return -EIO;
+  if (order_after_batches(c, s) != 0) return -EIO;
   // The ops in level order (call order within a level), cut into chunks;
   // each chunk carries the end of every level it holds part of.
   const uint32_t total = (uint32_t)c->ops.size();
@@ -908,18 +850,6 @@ bool in_reg(const oo_gpu_rx_ctx* c, const void* p, uint64_t bytes) {
   for (const HostReg& r : c->regs)
     if (a >= r.lo && a <= r.hi && bytes <= r.hi - a) return true;
   return false;
-}
-
-// The host address of [d, d + bytes) in a registered range, by its device
-// address (nullptr: not inside one).
-const void* host_of(const oo_gpu_rx_ctx* c, const void* d, uint64_t bytes) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(d);
-  for (const HostReg& r : c->regs) {
-    const uintptr_t dlo = reinterpret_cast<uintptr_t>(r.dev), len = r.hi - r.lo;
-    if (a >= dlo && a - dlo <= len && bytes <= len - (a - dlo))
-      return reinterpret_cast<const void*>(r.lo + (a - dlo));
-  }
-  return nullptr;
 }
 
 int alloc_host_slots(oo_gpu_rx_ctx* c) {
@@ -1104,8 +1034,7 @@ int oo_gpu_rx_close(oo_gpu_rx_ctx* c) {
     return 0;
   }
   (void)hipSetDevice(c->device);
-  if (c->h_bell != nullptr) __atomic_store_n(c->h_bell, oo_rx::RES_QUIT, __ATOMIC_RELEASE);
-  (void)hipDeviceSynchronize();  // every stream the context launched on (the resident kernel has left)
+  (void)hipDeviceSynchronize();  // every stream the context launched on
   free_dev(c);
   delete c;
   return 0;
@@ -1202,16 +1131,6 @@ int oo_gpu_rx_get_table_stats(oo_gpu_rx_ctx* c, oo_gpu_rx_table_stats* out) {
       hipMemcpy(&ok, c->T.kx_ok, sizeof(ok), hipMemcpyDeviceToHost) != hipSuccess)
     return -EIO;
   out->index_on = ok;
-  return 0;
-}
-
-int oo_gpu_rx_get_resident_stats(const oo_gpu_rx_ctx* c, oo_gpu_rx_resident_stats* out) {
-  if (c == nullptr || out == nullptr) return -EINVAL;
-  memset(out, 0, sizeof(*out));
-  out->batches = c->n_res;
-  out->fallbacks = c->n_res_fallback;
-  out->instances = c->res_epoch;
-  out->running = c->res_launched && c->res_seen && now_ns() - c->res_last_ns < kResUsableNs;
   return 0;
 }
 
@@ -1607,10 +1526,6 @@ static int launch(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t frames_bytes,
     A.done = n <= OO_POLL_DONE_MAX ? c->poll_done : nullptr;
     A.done_val = c->poll_done_val;
     A.rsvd = 0;
-    if (c->poll_h_desc != nullptr && n <= oo_rx::POLL_INLINE && P.ring_mask == ~0u) {
-      memcpy(A.d, c->poll_h_desc, sizeof(oo_gpu_pkt_desc) * n);
-      A.P.desc = nullptr;  // read from the kernel arguments
-    }
     rc = oo_rx_launch_poll(&A, grid, s);
     if (rc == 0 && A.done != nullptr) c->done_by_kernel = true;
   } else {
@@ -1748,14 +1663,8 @@ int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
     }
     (void)hipSetDevice(c->device);
     // No batch may still read it.
-    for (HostSlot& s : c->slot) {
-      if (!s.busy) continue;
-      if (s.res) {
-        if (!spin_done(s)) (void)res_recover(c, s);
-      } else {
-        (void)hipEventSynchronize(s.done);
-      }
-    }
+    for (HostSlot& s : c->slot)
+      if (s.busy) (void)hipEventSynchronize(s.done);
     // Only a stream that launched since its event was last recorded gets a
     // new one (it may since have been destroyed by a caller that did not
     // call oo_gpu_rx_stream_done); the others' events already
@@ -1774,97 +1683,6 @@ int oo_gpu_rx_host_unregister(oo_gpu_rx_ctx* c, void* p) {
     return 0;
   }
   return -ENOENT;
-}
-
-// ---- The resident poll kernel (oo_rx_kernel.hip "The resident poll
-// kernel").
-static int64_t now_ns() {
-  return std::chrono::duration_cast<std::chrono::nanoseconds>(
-             std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
-
-// Its stream, words and counters (made on the first eligible batch).
-static int res_init(oo_gpu_rx_ctx* c) {
-  if (c->h_bell != nullptr) return 0;
-  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
-  if (hipStreamCreateWithFlags(&c->res_s, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&c->h_mail), sizeof(oo_rx::ResMail) * oo_rx::RES_SLOTS, fl) !=
-          hipSuccess ||
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_mail), c->h_mail, 0) != hipSuccess ||
-      hipMalloc(&c->d_res_ctr, 128u * (2u + 2u * oo_rx::CLAIM_LINES)) != hipSuccess)
-    return -ENOMEM;
-  uint32_t* bell = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&bell), 256, fl) != hipSuccess) return -ENOMEM;
-  memset(bell, 0, 256);
-  c->h_bell = bell;
-  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_bell), c->h_bell, 0) != hipSuccess) return -EIO;
-  c->res_seq = 0;
-  return 0;
-}
-
-// Start an instance (the next epoch) on its stream, after the one before it
-// has left; it takes batches from the doorbell's current value on.  Its
-// counters and claim sets are zeroed first (stream order).
-static int res_start(oo_gpu_rx_ctx* c) {
-  if (res_init(c) != 0) return -ENOMEM;
-  KParams P;
-  memset(&P, 0, sizeof(P));
-  P.ring_mask = ~0u;
-  P.ip4_mask = c->ip4_mask;
-  P.ip6_mask = c->ip6_mask;
-  P.slot4 = c->T.slot4;
-  P.occ4 = c->T.occ4;
-  P.slot6 = c->T.slot6;
-  P.occ6 = c->T.occ6;
-  if (c->kx) {
-    P.kx4 = c->T.kx4;
-    P.kx6 = c->T.kx6;
-    P.kx_ok = c->T.kx_ok;
-    P.kx_nb4 = c->T.kx_nb4;
-    P.kx_ne6 = c->T.kx_ne6;
-  }
-  P.zero = c->d_zero;
-  P.sink = c->d_zero + 16u * oo_rx::ZERO_LINES;
-  P.stamps = nullptr;
-  P.hwport = c->d_zero + 16u * oo_rx::ZERO_LINES + oo_rx::SINK_BYTES;
-  // static tiles: the claims are made and ignored, in the instance's own sets
-  P.claim = c->d_res_ctr + 32u * 2u;
-  P.claim_next = P.claim + 32u * oo_rx::CLAIM_LINES;
-  P.ngroups = 1;
-  P.gshift = 0;
-  P.dyn = 0;
-  oo_rx::ResArgs A;
-  A.P = P;
-  A.doorbell = c->d_bell;
-  A.mail = c->d_mail;
-  A.ctr = c->d_res_ctr;
-  A.alive = c->d_bell + 32;
-  A.epoch = ++c->res_epoch;
-  A.seq0 = c->res_seq;
-  A.idle_ticks = kResIdleTicks;
-  const uint32_t wpb = (uint32_t)oo_rx_waves_per_block();
-  if (hipMemsetAsync(c->d_res_ctr, 0, 128u * (2u + 2u * oo_rx::CLAIM_LINES), c->res_s) != hipSuccess ||
-      oo_rx_launch_resident(&A, (int)(RES_WAVES / wpb), c->res_s) != 0)
-    return -EIO;
-  c->res_launched = true;
-  c->res_seen = false;
-  return 0;
-}
-
-// Whether a batch may be rung now: the instance launched last was seen
-// polling, and the last ring (or that sighting) is recent enough that it
-// cannot have idled out.  Otherwise a new instance is started (after the
-// old one leaves) and the batch takes the launch path.
-static bool res_usable(oo_gpu_rx_ctx* c, int64_t now) {
-  if (c->res_launched && !c->res_seen &&
-      __atomic_load_n(c->h_bell + 32, __ATOMIC_ACQUIRE) == c->res_epoch) {
-    c->res_seen = true;
-    c->res_last_ns = now;
-  }
-  if (c->res_launched && c->res_seen && now - c->res_last_ns < kResUsableNs) return true;
-  if (!c->res_launched || c->res_seen) (void)res_start(c);
-  return false;
 }
 
 // The slot's done word: written by the stream after everything the batch
@@ -1891,37 +1709,8 @@ static bool spin_done(const HostSlot& s) {
   }
 }
 
-// OO_DONE_EVENT: the slot's event polled instead (a runtime call per read).
-static bool spin_event(hipEvent_t e) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    const hipError_t r = hipEventQuery(e);
-    if (r == hipSuccess) return true;
-    if (r != hipErrorNotReady ||
-        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
-                .count() > kSpinNs)
-      return false;
-  }
-}
-
-// A resident batch whose done word did not come: stop the instance (quit,
-// its stream drained), and unless it took the batch after all, run the
-// batch through the launch path on the slot's stream and wait for it
-// (res_recover, below).
-
 static int complete_slot(oo_gpu_rx_ctx* c, HostSlot& s) {
-  if (s.res) {
-    if (!spin_done(s)) {
-      const int rc = res_recover(c, s);
-      if (rc < 0) {
-        s.busy = s.res = false;
-        return rc;
-      }
-    }
-    s.busy = s.res = false;
-    return (int)s.n;
-  }
-  if (!(OO_DONE_EVENT ? spin_event(s.done) : spin_done(s)) && hipEventSynchronize(s.done) != hipSuccess) {
+  if (!spin_done(s) && hipEventSynchronize(s.done) != hipSuccess) {
     s.busy = false;
     return -EIO;
   }
@@ -1930,32 +1719,6 @@ static int complete_slot(oo_gpu_rx_ctx* c, HostSlot& s) {
   s.busy = false;
   (void)c;
   return (int)s.n;
-}
-
-static int res_recover(oo_gpu_rx_ctx* c, HostSlot& s) {
-  ++c->n_res_fallback;
-  __atomic_store_n(c->h_bell, oo_rx::RES_QUIT, __ATOMIC_RELEASE);
-  if (hipStreamSynchronize(c->res_s) != hipSuccess) return -EIO;  // (it leaves between batches)
-  __atomic_store_n(c->h_bell, c->res_seq, __ATOMIC_RELEASE);        // the next instance starts here
-  c->res_launched = c->res_seen = false;
-  if (*reinterpret_cast<const volatile uint32_t*>(s.h_done) == done_word(s.ticket)) return 0;
-  // On the tables as the device holds them now (queued changes stay queued:
-  // the batch was submitted before them).
-  hipStream_t st = s.stream;
-  if (c->tables_gen != 0 && hipStreamWaitEvent(st, c->tables_ev, 0) != hipSuccess) return -EIO;
-  if (launch(c, s.r_frames, s.r_frames_bytes, s.r_desc, s.n, s.r_out, nullptr, st) != 0 ||
-      hipStreamWriteValue32(st, s.d_done, done_word(s.ticket), 0) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return -EIO;
-  return 0;
-}
-
-// Every batch rung to the resident kernel has completed (table changes wait
-// for them, as for the batches on streams).
-static int res_quiesce(oo_gpu_rx_ctx* c) {
-  for (HostSlot& s : c->slot)
-    if (s.busy && s.res && !spin_done(s) && res_recover(c, s) != 0) return -EIO;
-  return 0;
 }
 
 int oo_gpu_rx_submit(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes,
@@ -2003,7 +1766,7 @@ int oo_gpu_rx_submit(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes
   }
   ok = ok && hipMemcpyAsync(s.h_ctr, s.d_ctr, sizeof(oo_gpu_rx_counters), hipMemcpyDeviceToHost,
                             st) == hipSuccess &&
-       (OO_DONE_EVENT || hipStreamWriteValue32(st, s.d_done, done_word(t), 0) == hipSuccess) &&
+       hipStreamWriteValue32(st, s.d_done, done_word(t), 0) == hipSuccess &&
        hipEventRecord(s.done, st) == hipSuccess;
   if (!ok) return -EIO;
   s.busy = true;
@@ -2033,71 +1796,20 @@ int oo_gpu_rx_submit_mapped(oo_gpu_rx_ctx* c, const void* d_frames, uint64_t fra
   }
   hipStream_t st = s.stream;
   bool by_kernel = false;  // the poll instance writes the done word itself
-  if (n > 0 && n <= OO_RES_MAX && c->kmode == 0 && c->grid_poll > 0) {
-    const int64_t now = now_ns();
-    if (res_usable(c, now)) {
-      int rc = prepare(c, st);
-      if (rc) return rc;
-      const bool tables = c->tables_gen != c->res_tables_gen;
-      if (tables) {  // the flush (or the wait for one) on st has run
-        if (hipStreamSynchronize(st) != hipSuccess) return -EIO;
-        c->res_tables_gen = c->tables_gen;
-      }
-      // The static partition of rx_kernel's small batches over RES_WAVES waves.
-      const uint64_t W = RES_WAVES, step = c->tstep;
-      const uint64_t K = (n + 64 * W - 1) / (64 * W);
-      const uint64_t NT = std::max<uint64_t>(1, std::min<uint64_t>(W * K, n / 8));
-      const uint64_t tlo = std::min<uint64_t>(64 - step, (n / NT) / step * step);
-      const uint32_t seq = c->res_seq + 1u;
-      oo_rx::ResMail& m = c->h_mail[seq % oo_rx::RES_SLOTS];
-      m.frames = reinterpret_cast<uint64_t>(d_frames);
-      m.frames_bytes = frames_bytes;
-      m.desc = reinterpret_cast<uint64_t>(d_desc);
-      m.out = reinterpret_cast<uint64_t>(d_out);
-      m.done = reinterpret_cast<uint64_t>(s.d_done);
-      m.n = n;
-      m.ntiles = (uint32_t)NT;
-      m.tlo = (uint32_t)tlo;
-      m.ta = (uint32_t)std::min<uint64_t>(NT, (n - tlo * NT) / step);
-      m.tstep = (uint32_t)step | (tables ? oo_rx::RES_TABLES : 0u);
-      m.done_val = done_word(t);
-      __atomic_store_n(c->h_bell, seq, __ATOMIC_RELEASE);  // (the mailbox before it)
-      c->res_seq = seq;
-      c->res_last_ns = now;
-      ++c->n_res;
-      c->last_path = 6u;
-      s.res = true;
-      s.r_frames = d_frames;
-      s.r_frames_bytes = frames_bytes;
-      s.r_desc = d_desc;
-      s.r_out = d_out;
-      s.busy = true;
-      s.ticket = t;
-      s.n = n;
-      s.out = d_out;
-      s.delta = nullptr;
-      s.copy_out = false;
-      c->next_ticket = t + 1;
-      *ticket = t;
-      return 0;
-    }
-  }
   if (n > 0) {
     int rc = prepare(c, st);
     if (rc == 0) {
       c->poll_done = s.d_done;
       c->poll_done_val = done_word(t);
-      c->poll_h_desc = static_cast<const oo_gpu_pkt_desc*>(host_of(c, d_desc, sizeof(oo_gpu_pkt_desc) * n));
       c->done_by_kernel = false;
       rc = launch(c, d_frames, frames_bytes, d_desc, n, d_out, nullptr, st);
       by_kernel = rc == 0 && c->done_by_kernel;
       c->poll_done = nullptr;
-      c->poll_h_desc = nullptr;
       c->done_by_kernel = false;
     }
     if (rc) return rc;
   }
-  if ((!by_kernel && !OO_DONE_EVENT && hipStreamWriteValue32(st, s.d_done, done_word(t), 0) != hipSuccess) ||
+  if ((!by_kernel && hipStreamWriteValue32(st, s.d_done, done_word(t), 0) != hipSuccess) ||
       hipEventRecord(s.done, st) != hipSuccess)
     return -EIO;
   s.busy = true;

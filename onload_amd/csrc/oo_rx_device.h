@@ -263,51 +263,14 @@ struct KParams {
 };
 
 // The poll instance's kernel arguments (oo_rx_kernel.hip "The poll
-// instance"): the batch's KParams, its completion (done null: none) and, for
-// a batch of at most POLL_INLINE packets launched with P.desc null, its
-// descriptors.  Off by default (OO_POLL_INLINE 0: 16 B of them): with 128
-// descriptors the arguments are 2.3 KiB a launch, and the GPU faults of this
-// round came only with such launches in the process;
-// the saving was ~1 us a poll.
-#ifndef OO_POLL_INLINE
-#define OO_POLL_INLINE 0
-#endif
-constexpr uint32_t POLL_INLINE = OO_POLL_INLINE;
+// instance"): the batch's KParams and its completion (done null: none).
 struct PollArgs {
   KParams P;
   uint32_t* done_ctr;  // the launch's claim-set FLAG_LINE word (0 at launch)
   uint32_t* done;      // host-mapped word: done_val once every record has landed
   uint32_t done_val;
   uint32_t rsvd;
-  oo_gpu_pkt_desc d[POLL_INLINE > 0 ? POLL_INLINE : 1];
 };
-constexpr uint64_t POLL_DESC_OFF = offsetof(PollArgs, d);
-
-// The resident poll kernel (oo_rx_kernel.hip "The resident poll kernel"):
-// one mailbox per batch in host memory, written before the doorbell.
-struct ResMail {
-  uint64_t frames, frames_bytes;
-  uint64_t desc;      // the batch's descriptors (device address)
-  uint64_t out;       // its records (device address of host memory)
-  uint64_t done;      // the slot's done word (device address of host memory)
-  uint32_t n, ntiles, tlo, ta;
-  uint32_t tstep;     // | RES_TABLES: the tables changed since the last batch
-  uint32_t done_val;
-};
-static_assert(sizeof(ResMail) == 64, "one 64-B mailbox line");
-constexpr uint32_t RES_SLOTS = 4;           // mailboxes (batch seq mod RES_SLOTS)
-constexpr uint32_t RES_QUIT = 0xffffffffu;  // doorbell value: leave the loop
-constexpr uint32_t RES_TABLES = 0x80000000u;
-struct ResArgs {
-  KParams P;                 // tables, zero lines, claim sets; per batch fields from the mailbox
-  const uint32_t* doorbell;  // host memory: the last batch sequence number rung
-  const ResMail* mail;       // host memory: RES_SLOTS mailboxes
-  uint32_t* ctr;             // device: two counters 128 B apart (batch parity), 0 at launch
-  uint32_t* alive;           // host memory: the instance's epoch once it polls
-  uint32_t epoch, seq0;      // this instance; the doorbell value it starts from
-  uint64_t idle_ticks;       // s_memrealtime ticks (100 MHz) without a batch before it leaves
-};
-static_assert(POLL_DESC_OFF % 16 == 0 && sizeof(PollArgs) <= 4096, "PollArgs layout");
 
 }  // namespace oo_rx
 

@@ -2035,20 +2035,9 @@ __device__ __forceinline__ DescView desc_view(const KParams& P, const uint4& d, 
 
 // Where lane `lane` of unit t loads its descriptor from (lanes without a
 // packet: some other in-bounds entry).
-#ifdef OO_RX_POLL
-// The poll instance: a batch of at most POLL_INLINE packets may bring its
-// descriptors in the kernel arguments (P.desc null: PollArgs::d), read from
-// where the launch put them instead of over PCIe from the caller's memory.
-__device__ __forceinline__ uint64_t desc_base(const KParams& P) {
-  return P.desc != nullptr
-             ? reinterpret_cast<uint64_t>(P.desc)
-             : reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + POLL_DESC_OFF;
-}
-#else
 __device__ __forceinline__ uint64_t desc_base(const KParams& P) {
   return reinterpret_cast<uint64_t>(P.desc);
 }
-#endif
 __device__ __forceinline__ uint64_t desc_at(const KParams& P, uint32_t i) {
   return desc_base(P) + (uint64_t)((P.ring_cons + i) & P.ring_mask) * 16;
 }
@@ -2382,6 +2371,22 @@ constexpr int NST = 2;
 constexpr int E = OO_RX_EXTRA;
 static_assert(E % 2 == 0 && E <= HC, "extra rounds live in the header rows");
 
+// The deep ring (OO_RX_DEEP, rx_kernel only): once the parse has read the
+// header rows, the R ring rows and the HC header rows are one ring of
+// S = R + HC slots for the whole body, not only for E extra rounds -- round k
+// in row (k + HC) mod S -- and each header row takes its window of the next
+// tile when its last round of this tile has been consumed (a row no round
+// reaches takes it right after the demux).  Every tile keeps S rounds in
+// flight through its body where the plain loop keeps R after its first
+// R + E, at the price of the next tile's windows landing during this tile's
+// last rounds instead of during its whole body.
+// The waits are counted from each slot's issue index (a lane of one VGPR),
+// so they hold for any mix of refills and window rows.
+#ifndef OO_RX_DEEP
+#define OO_RX_DEEP 0
+#endif
+constexpr int S_DEEP = R + HC;
+
 struct WaveLds {
   uint4 hdr[HC][64];            // header windows (stage_window)
   uint4 ring[R][64];            // body ring: slot = one round of the eight groups
@@ -2437,9 +2442,9 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
   const uint32_t hi = lane & 1u;
   const uint32_t last = t.cnt - 1u;
-  // (a global pointer whatever P.out came from: the resident kernel reads
-  // it from host memory, where a generic pointer would make these flat
-  // stores, counted in lgkmcnt as well)
+  // (a global pointer whatever P.out came from -- HBM or host-mapped
+  // records: a generic pointer would make these flat stores, counted in
+  // lgkmcnt as well)
   __attribute__((address_space(1))) u32x4* const out =
       (__attribute__((address_space(1))) u32x4*)reinterpret_cast<uintptr_t>(P.out);
 #pragma unroll
@@ -2570,8 +2575,31 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // and after the demux: issued before it they are older than its loads,
     // and every demux wait would wait for them too (configs 2/4/5 -1.7 /
     // -0.5 / -0.7 %, profiles/r04/ab_extra_after_demux.log).
+    // The deep ring: header row h's window of the next tile (packet p's
+    // cell c for lane (p & 7, c), as stage_window lays it out), its
+    // descriptor read from LDS by the lane itself.
+    constexpr bool DEEP = OO_RX_DEEP && !TX && E == HC;
+    auto window_row = [&](uint32_t h) {
+      const Unit nt = unit_of(P, tnext);
+      const uint32_t p = h * 8u + (lane >> 3);
+      const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][p]), nt, p);
+      const uint32_t c = ((lane & 7u) + p) & 7u;
+      const int nwin = (dn.span + 15) >> 4;
+      glds<OO_RX_HDR_AUX>((int)c < nwin ? dn.abase + (uint64_t)c * 16 : zero_line(P, nt, lane),
+                          &L.hdr[h][0]);
+    };
     auto issue_extra = [&]() {
-      if (ext) {
+      if constexpr (DEEP) {
+        // Rounds R..S-1 into the header rows, in order; a row no round of
+        // this tile reaches takes its next-tile window now.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t t0 = sreg(lds_read4(&L.T0));
+#pragma unroll
+        for (int u = 0; u < HC; ++u) {
+          if ((uint32_t)(R + u) < t0) issue_round(ci, J, zero, &L.hdr[u][0], lane);
+          else window_row((uint32_t)u);
+        }
+      } else if (ext) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int u = 0; u < E; ++u) issue_round(ci, J, zero, &L.hdr[u][0], lane);
@@ -2623,7 +2651,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
     };
-    if (!ext) stage_next();
+    if (!DEEP && !ext) stage_next();
 
     claim_tile(P.claim + sreg(lds_read4(&L.gofs)), P.ngroups, lane, got);  // tile i + 3
 
@@ -2637,10 +2665,47 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       cc.bs = 0;
     }
 
+    if constexpr (DEEP) {
+      // Issue indices since the tile's start: slot s (round s's, or for a
+      // header row no round reached, its window) was op s + 1; then the
+      // descriptor line and the claim.  Round k's slot is k mod S; waiting
+      // for it leaves the ops issued after it outstanding.
+      constexpr uint32_t S = (uint32_t)S_DEEP;
+      uint32_t rs = lane + 1u;  // lane s: issue index of slot s's op
+      uint32_t q = S + 2u;      // ops issued so far
+      uint32_t s0 = 0;          // slot of round k
+      for (uint32_t k = 0; k < T0; k += 2, s0 = s0 + 2u == S ? 0u : s0 + 2u) {
+        const uint32_t s1 = s0 + 1u;  // (S even: a pair never wraps)
+        const uint32_t idx = (uint32_t)__builtin_amdgcn_readlane((int)rs, (int)(k + 1u < T0 ? s1 : s0));
+        vm_wait_n((int)(q - idx));
+        const uint32_t r0 = s0 < (uint32_t)R ? s0 + HC : s0 - R;
+        const uint32_t r1 = s1 < (uint32_t)R ? s1 + HC : s1 - R;
+        uint4 v0, v1;  // (round T0, past the end when T0 is odd: weighed 0)
+        lds_read16x2(&L.hdr[r0][lane], &L.hdr[r1][lane], v0, v1);
+        consume_round(cc, J, v0, lane);
+        consume_round(cc, J, v1, lane);
+        // The two slots: their next round, else (a header row) the next
+        // tile's window, else nothing.
+#pragma unroll
+        for (uint32_t d = 0; d < 2u; ++d) {
+          const uint32_t j = k + d, s = s0 + d, row = d ? r1 : r0;
+          if (j >= T0) continue;
+          if (j + S < T0) {
+            issue_round(ci, J, zero, &L.hdr[row][0], lane);
+            rs = lane == s ? q + 1u : rs;
+            ++q;
+          } else if (s >= (uint32_t)R) {
+            window_row(row);
+            ++q;
+          }
+        }
+      }
+    }
+
     // ---- body stream, two pieces per step.  Each wait counts the
     // operations issued after the awaited pair (the demux loads excepted:
     // the demux waited for its last one, and with it for everything older).
-    if (ext) {
+    if (!DEEP && ext) {
       // Ring rounds 0..R-1, refilled with R+E..R+E+R-1: newer than the
       // pair, the rest of the ring, the E header-row rounds, the descriptor
       // line and the claim, and the refills so far -- R + E in all.
@@ -2670,7 +2735,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // rest of the ring, plus in the first turn the staging operations issued
     // since the ring was filled (NHS, or HC after an ext prefix); none past T.
     const int nhs = ext ? HC : NHS;
-    for (uint32_t k0 = 0; k0 < T; k0 += R) {
+    for (uint32_t k0 = 0; k0 < (DEEP ? 0u : T); k0 += R) {
       const bool first = k0 == 0, last = k0 + R == T;
 #pragma unroll
       for (int u = 0; u < R; u += 2) {
@@ -2730,8 +2795,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
 // PCIe, is bound by its chain of round trips, not by bytes.  The same tile
 // loop, with a ring deep enough (OO_RX_RING 12) that a tile of eight
 // 1514-B frames issues its whole body with its header windows -- one round
-// trip for the frames, where the 4-slot ring waits three -- its descriptors
-// from the kernel arguments when they fit there (desc_base), and its own
+// trip for the frames, where the 4-slot ring waits three -- and its own
 // completion: each wave, once its record stores have completed, counts
 // itself in the launch's claim-set FLAG_LINE word (zeroed by the stream's
 // previous launch), and the last one writes the caller's done word in host
@@ -2754,90 +2818,6 @@ __global__ __launch_bounds__(WAVES * 64) void rx_kernel(PollArgs A) {
   if (A.done != nullptr) poll_done(A);
 }
 
-// ---------------------------------------------------------------------------
-// The resident poll kernel: the poll instance's tile
-// loop run for batch after batch by a small grid that stays on the device,
-// so a poll's batch pays no launch.  The host writes batch k's mailbox
-// (ResMail: frames, descriptors, records, partition, the slot's done word)
-// and then the doorbell = k.  In each block one lane polls the doorbell in
-// host memory (sleeping between reads) and the block's waves run every batch
-// up to the value read, in order; per batch each wave with a tile counts
-// itself out as poll_done does (counter by batch parity; the last resets the
-// other parity's counter before it writes the done word).  A mailbox flagged with
-// a table change (RES_TABLES in its tstep word) makes each wave drop its
-// cached table lines first (agent-scope acquire).  Every block leaves once the doorbell reads
-// RES_QUIT or after idle_ticks without a new batch: the host rings only
-// while well inside that window (oo_gpu_rx.cpp res_usable), so no block
-// leaves with a batch outstanding.
-__device__ __forceinline__ uint64_t mail_word2(const uint32_t (&w)[16], int k) {
-  return (uint64_t)w[k] | ((uint64_t)w[k + 1] << 32);
-}
-
-__global__ __launch_bounds__(WAVES * 64) void rx_resident(ResArgs A) {
-  __shared__ uint32_t s_bell;
-  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_store(A.alive, A.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  uint32_t seen = A.seq0;
-  uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    if (threadIdx.x == 0) {
-      uint32_t v;
-      for (;;) {
-        v = __hip_atomic_load(A.doorbell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (v != seen) break;
-        if (__builtin_amdgcn_s_memrealtime() - t_idle > A.idle_ticks) {
-          v = RES_QUIT;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      s_bell = v;
-    }
-    __syncthreads();
-    const uint32_t bell = s_bell;
-    __syncthreads();  // (s_bell is rewritten only after every wave read it)
-    if (bell == RES_QUIT) break;
-    while (seen != bell) {
-      ++seen;
-      // The batch's mailbox: lanes 0..15 read its sixteen words (system
-      // scope: from host memory, after the doorbell).
-      const uint32_t* const mw = reinterpret_cast<const uint32_t*>(A.mail + seen % RES_SLOTS);
-      const uint32_t mv =
-          __hip_atomic_load(mw + (lane & 15u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      uint32_t w[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = (uint32_t)__builtin_amdgcn_readlane((int)mv, k);
-      if (w[14] & RES_TABLES) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      KParams P = A.P;
-      P.frames = reinterpret_cast<const uint8_t*>(mail_word2(w, 0));
-      P.frames_bytes = mail_word2(w, 2);
-      P.desc = reinterpret_cast<const oo_gpu_pkt_desc*>(mail_word2(w, 4));
-      P.out = reinterpret_cast<oo_gpu_rx_result*>(mail_word2(w, 6));
-      P.n = w[10];
-      P.ntiles = w[11];
-      P.tlo = w[12];
-      P.ta = w[13];
-      P.tstep = w[14] & 0xffu;
-      tile_loop<false>(P);
-      // Counted out (poll_done, by batch parity): the waves that had a tile
-      // (waves 0 .. ntiles-1; ntiles <= the grid's waves), so the done word
-      // does not wait for blocks that saw the doorbell late and had nothing.
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t gw = blockIdx.x * (uint32_t)WAVES + (threadIdx.x >> 6);
-      if (lane == 0 && gw < P.ntiles) {
-        uint32_t* const ctr = A.ctr + 32u * (seen & 1u);
-        const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (prev + 1u == P.ntiles) {
-          __hip_atomic_store(A.ctr + 32u * ((seen + 1u) & 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)mail_word2(w, 8), w[15],
-                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-    }
-    t_idle = __builtin_amdgcn_s_memrealtime();
-  }
-}
 #else
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void rx_kernel(KParams P) {
   tile_loop<false>(P);
@@ -3399,12 +3379,6 @@ extern "C" int oo_rx_launch_poll(const oo_rx::PollArgs* A, int grid, hipStream_t
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Start the resident poll kernel on `stream` (it stays until the doorbell
-// reads RES_QUIT or it has idled for A->idle_ticks).
-extern "C" int oo_rx_launch_resident(const oo_rx::ResArgs* A, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(oo_rx_poll::rx_resident, dim3(grid), dim3(oo_rx_poll::WAVES * 64), 0, stream, *A);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 #elif defined(OO_RX_SHORT)
 // Resident blocks per CU of the short-frame rx_kernel.
 extern "C" int oo_rx_blocks_per_cu_short(void) {

@@ -207,20 +207,10 @@ class GpuRxStack:
             raise OSError(-rc, "oo_gpu_rx_get_table_stats")
         return {n: int(getattr(st, n)) for n, _ in st._fields_ if n != "rsvd"}
 
-    def resident_stats(self) -> dict:
-        """oo_gpu_rx_get_resident_stats: batches the resident poll kernel
-        took, of them re-run through a launch, instances started, running."""
-        st = _abi.ResidentStats()
-        rc = self._lib.oo_gpu_rx_get_resident_stats(self._ctx, ctypes.byref(st))
-        if rc:
-            raise OSError(-rc, "oo_gpu_rx_get_resident_stats")
-        return {n: int(getattr(st, n)) for n, _ in st._fields_}
-
     def last_path(self) -> int:
         """oo_gpu_rx_last_path: the last batch's kernels (1 / 2 rx_kernel
         instances, 3 / 4 the split transform with the lockstep / sequences
-        body engine, 5 the poll instance, 6 the resident poll kernel, 0 none
-        yet)."""
+        body engine, 5 the poll instance, 0 none yet)."""
         return int(self._lib.oo_gpu_rx_last_path(self._ctx))
 
     def set_len_hint(self, mean_frame_len: int) -> None:

@@ -350,22 +350,21 @@ static void dispatch(oo_rx_poll* p, uint32_t id, const uint8_t* frame,
 
 /* The crossover's cost model (oo_rx_poll.h): whether the device batch of m
  * frames and `bytes` frame bytes costs less than the caller's per-event
- * path.  The defaults are tools/poll_bench's fits on MI355X boxes
- * (DESIGN.md §5e, round 5): the per-event path 20.3 ns per frame + 0.146 ns
- * per byte on one host core; a device batch ~18.5 us fixed (launch, PCIe
- * and HBM round trips, the completion word) + 15 ns per frame, + 0.023 ns
- * per byte read in place (zero copy) or 0.081 ns per byte gathered (the
- * host memcpy).  (A library built with the poll instance and the resident
- * kernel, DESIGN.md §5e, fits 13.5 us, 25 ns, 0.011 / 0.058 ns: set them in
- * oo_rx_poll_cfg.) */
+ * path.  The defaults are tools/poll_bench's fit on an MI355X box
+ * (profiles/r06/poll_latency_product.jsonl): the
+ * per-event path 21.3 ns per frame + 0.121 ns per byte on one host core; a
+ * device batch (the poll instance up to 256 frames) ~17.4 us fixed
+ * (launch, PCIe and HBM round trips, the completion word) + 15 ns per
+ * frame, + 0.019 ns per byte read in place (zero copy) or 0.075 ns per byte
+ * gathered (the host memcpy). */
 static int gpu_pays(const oo_rx_poll* p, uint64_t m, uint64_t bytes)
 {
   const oo_rx_poll_cfg* c = &p->cfg;
-  const uint64_t cpu_pkt = c->cpu_pkt_ps ? c->cpu_pkt_ps : 20300;
-  const uint64_t cpu_byte = c->cpu_byte_ps ? c->cpu_byte_ps : 146;
-  const uint64_t fixed = (uint64_t)(c->gpu_fixed_ns ? c->gpu_fixed_ns : 18500) * 1000u;
+  const uint64_t cpu_pkt = c->cpu_pkt_ps ? c->cpu_pkt_ps : 21300;
+  const uint64_t cpu_byte = c->cpu_byte_ps ? c->cpu_byte_ps : 121;
+  const uint64_t fixed = (uint64_t)(c->gpu_fixed_ns ? c->gpu_fixed_ns : 17400) * 1000u;
   const uint64_t gpu_pkt = c->gpu_pkt_ps ? c->gpu_pkt_ps : 15000;
-  const uint64_t gpu_byte = c->gpu_byte_ps ? c->gpu_byte_ps : (p->zero_copy ? 23 : 81);
+  const uint64_t gpu_byte = c->gpu_byte_ps ? c->gpu_byte_ps : (p->zero_copy ? 19 : 75);
   return fixed + m * gpu_pkt + bytes * gpu_byte < m * cpu_pkt + bytes * cpu_byte;
 }
 

@@ -72,10 +72,8 @@ def test_poll_dispatch_and_counters(cuda, sw_verify, evs_per_poll, seed):
         assert a == b, (k, a, b)
     st = p.stats.as_dict()
     assert onload_stats(st) == want
-    rs = g.resident_stats()
-    if rs["instances"]:  # a library built with the resident poll kernel on
-        assert evs_per_poll > 200 or rs["batches"] > 0, rs
-        assert rs["fallbacks"] == 0, rs
+    if evs_per_poll <= 256 and st["n_batches"]:  # a poll's batch: the poll instance
+        assert g.last_path() == 5
     ntrans = len(want_recs)
     assert st["n_batches"] == (0 if ntrans == 0 else
                                sum(1 for s in range(0, len(evs), evs_per_poll)

@@ -135,30 +135,6 @@ def test_poll_kernel_same_invariants(asm_poll):
     assert "tx_kernel" not in text and "win_kernel" not in text
 
 
-RES = "_ZN10oo_rx_poll11rx_residentEN5oo_rx7ResArgsE"
-
-
-def test_resident_kernel_invariants(asm_poll):
-    """The resident poll kernel: no scratch; per batch the tile loop's two
-    record stores and zero_claim_set's three, the batch-parity counter reset
-    (`sc1`), and two system-scope stores (`sc0 sc1`): the done word and, once
-    per instance, the alive word; one returning system-scope add per wave and
-    batch; the doorbell read in a loop that also leaves on a deadline
-    (s_memrealtime) and sleeps between reads."""
-    text, stderr = asm_poll
-    u = _usage(stderr, RES)
-    assert u["VGPRs Spill"] == 0, u
-    rx = _body(text, RES)
-    assert "scratch_" not in rx
-    assert len(re.findall(r"global_store_dwordx4", rx)) == 2
-    assert not re.findall(r"global_store_(byte|short|dwordx2)", rx)
-    assert len(re.findall(r"global_store_dword .* sc0 sc1$", rx, re.M)) == 2
-    assert len(re.findall(r"global_store_dword .* sc1$", rx, re.M)) == 6
-    assert len(re.findall(r"global_atomic_add .* sc0 sc1$", rx, re.M)) == 1
-    assert "s_memrealtime" in rx and "s_sleep" in rx
-    assert not re.findall(r"flat_store|flat_load|flat_atomic", rx)
-
-
 WIN = "_ZN5oo_rx10win_kernelENS_7KParamsE"
 BODY = "_ZN5oo_rx11body_kernelENS_7KParamsE"
 

@@ -13,7 +13,6 @@
 #   ta        texture-path pass (TA/TD/TCP) -> ta_c<N>/
 #   ab        same-box A/B of LIBS entries (tools/ab.sh) -> ab.log
 #   poll      tools/poll_bench per poll size (EPP) -> poll.jsonl
-#   pollab    tools/poll_ab.sh over VARIANTS (make poll-variants) -> poll_ab.jsonl
 #   stamps    the OO_RX_STAMPS build on STAMP_CONFIG via tools/stamps.py
 # Every GPU step runs under its own time limit; the first failure ends the
 # call (no retries).  Output under gpurun_out/$TAG (default "round").
@@ -103,13 +102,6 @@ for step in ${STEPS:-tests bench}; do
 for l in open("'"$OUT"'/poll.jsonl"):
     d = json.loads(l)
     print({k: d.get(k) for k in ("config", "evs_per_poll", "mode", "poll_us_median", "mpps", "cpu_poll_us_equiv", "handed_back", "fit")})' ;;
-    pollab)
-      VARIANTS="${VARIANTS:-base}" bash tools/poll_ab.sh > "$OUT/poll_ab.jsonl" 2> "$OUT/poll_ab.err" \
-        || fail pollab $? "$OUT/poll_ab.err"
-      python3 -c 'import json
-for l in open("'"$OUT"'/poll_ab.jsonl"):
-    d = json.loads(l)
-    if d["mode"] == "zero_copy": print(d["variant"], d["config"], d["evs_per_poll"], d["poll_us_median"], d["cpu_poll_us_equiv"])' ;;
     stamps)
       OO_RX_LIB="${OO_RX_LIB:-build/var_st.so}" timeout -k 10 300 python tools/stamps.py --config ${STAMP_CONFIG:-3} \
         > "$OUT/stamps.txt" 2> "$OUT/stamps.err" \
