@@ -261,6 +261,7 @@ struct oo_gpu_rx_ctx {
   uint32_t* h_kx_req = nullptr;
   uint32_t* d_kx_req = nullptr;
   uint64_t n_flush = 0, n_kx_full = 0, n_kx_inc = 0;
+  uint64_t n_kx_inc_run = 0;  // incremental updates since the last rebuild
   Tracked track[NTRACK];
   uint64_t lru = 0;
   uint8_t* d_zero = nullptr;   // oo_rx::ZERO_LINES x 16 B of zeros, the sink, the hwport table
@@ -301,7 +302,9 @@ struct oo_gpu_rx_ctx {
   hipEvent_t len_ev = nullptr;
   const void* len_desc = nullptr;
   uint32_t len_n = 0, len_cons = 0, len_seq = 0;
+  uint32_t len_uses = 0;       // launches on the sampled key since its sample
   bool len_pending = false;
+  bool host_batch = false;     // launch() runs oo_gpu_rx_submit's batch: no sample
   int len_mixed = -1;          // the sampled batch: 1 mixed sizes, 0 not, -1 not known yet
   uint32_t tstep = 8;          // tile size step (KParams::tstep)
   uint64_t* stamps = nullptr;  // diagnostic phase stamps (OO_RX_STAMPS builds)
@@ -751,8 +754,18 @@ void mark_kx_owners(TableOp* h, uint32_t n) {
 // after the first chunk has been enqueued leaves the device tables in an
 // unknown state: the context then refuses every later call (-EIO) rather
 // than apply the queued ops twice.
+// With no ops queued it only rebuilds the key index (index_due): the
+// index asked for it, or has had kKxIncMax incremental updates since its
+// last rebuild (a key that lost its last match keeps a KX_DEAD entry, whose
+// lookups walk: ADVICE r5).
+constexpr uint64_t kKxIncMax = 256;
+bool index_due(const oo_gpu_rx_ctx* c) {
+  if (c->T.kx4 == nullptr || c->h_kx_req == nullptr) return false;
+  return *reinterpret_cast<const volatile uint32_t*>(c->h_kx_req) != 0 || c->n_kx_inc_run >= kKxIncMax;
+}
+
 int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
-  if (c->ops.empty()) return 0;
+  if (c->ops.empty() && !index_due(c)) return 0;
   if (order_after_batches(c, s) != 0) return -EIO;
   // The ops in level order (call order within a level), cut into chunks;
   // each chunk carries the end of every level it holds part of.
@@ -765,8 +778,8 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
   // rebuild updates the index for the ops' keys.
   const bool small = total <= oo_table_threads();
   const bool req = c->h_kx_req != nullptr && *reinterpret_cast<volatile uint32_t*>(c->h_kx_req) != 0;
-  const bool inc = small && !c->kx_full && !c->ops_sock && !req && c->d_kx_req != nullptr &&
-                   c->T.kx4 != nullptr;
+  const bool inc = total > 0 && small && !c->kx_full && !c->ops_sock && !req &&
+                   c->n_kx_inc_run < kKxIncMax && c->d_kx_req != nullptr && c->T.kx4 != nullptr;
   for (uint32_t at = 0; at < total; at += OPS_CHUNK) {
     const uint32_t n = std::min(OPS_CHUNK, total - at);
     OpStage& st = c->stage[c->stage_next];
@@ -807,10 +820,13 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
     c->failed = true;
     return -EIO;
   }
-  ++c->n_flush;
+  if (total > 0) ++c->n_flush;
   ++(inc ? c->n_kx_inc : c->n_kx_full);
-  clear_ops(c);
-  ++c->gen;
+  c->n_kx_inc_run = inc ? c->n_kx_inc_run + 1 : 0;
+  if (total > 0) {
+    clear_ops(c);
+    ++c->gen;
+  }
   ++c->tables_gen;
   Tracked* t = track_of(c, s);
   if (t == nullptr || hipEventRecord(c->tables_ev, s) != hipSuccess) {
@@ -826,7 +842,7 @@ int flush_ops(oo_gpu_rx_ctx* c, hipStream_t s) {
 // last flush when it ran on another stream.  Returns s's tracked entry.
 int prepare(oo_gpu_rx_ctx* c, hipStream_t s, Tracked** out = nullptr) {
   if (c->failed) return -EIO;
-  if (!c->ops.empty()) {
+  if (!c->ops.empty() || index_due(c)) {
     const int rc = flush_ops(c, s);
     if (rc) return rc;
   }
@@ -1291,7 +1307,11 @@ static void set_tiles_dyn(KParams& P, uint32_t n, uint64_t W, uint32_t S, uint32
 // Whether a launch's batch has the sampled mixed-size profile: the same
 // descriptors (address, count, ring position) as the last sampled batch, and
 // that sample landed.  No caller hint (a hint names the frames' mean size
-// only).
+// only).  The key names a buffer, not its contents: a caller that refills
+// one descriptor buffer gets a fresh sample every kLenResample launches on
+// it (sample_lengths), so the choice follows a changed mix within that many
+// batches.  (The choice never changes the records, only which kernels run.)
+constexpr uint32_t kLenResample = 64;
 static bool mixed_sizes(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n) {
   if (c->len_hint != 0 || c->h_len == nullptr) return false;
   if (c->len_desc != static_cast<const void*>(P.desc) || c->len_n != n || c->len_cons != P.ring_cons)
@@ -1315,13 +1335,20 @@ static bool mixed_sizes(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n) {
 static void sample_lengths(oo_gpu_rx_ctx* c, const KParams& P, uint32_t n, hipStream_t s) {
   // (only batches the profile can change the choice of: a poll's small
   // batches would pay a launch for nothing)
-  if (c->len_hint != 0 || c->h_len == nullptr || c->kmode != 0 || n < (1u << 16)) return;
-  if (c->len_desc == static_cast<const void*>(P.desc) && c->len_n == n && c->len_cons == P.ring_cons)
+  // (nor the host path's batches: its two staging slots alternate their
+  // descriptor buffers, so every batch would be a new key, sampled and never
+  // used -- ADVICE r5; a caller wanting the mixed-size choice there passes
+  // a hint)
+  if (c->len_hint != 0 || c->h_len == nullptr || c->kmode != 0 || n < (1u << 16) || c->host_batch)
     return;
+  const bool same =
+      c->len_desc == static_cast<const void*>(P.desc) && c->len_n == n && c->len_cons == P.ring_cons;
+  if (same && ++c->len_uses < kLenResample) return;
+  c->len_uses = 0;
   c->len_desc = P.desc;
   c->len_n = n;
   c->len_cons = P.ring_cons;
-  c->len_mixed = -1;
+  if (!same) c->len_mixed = -1;  // (a resample keeps the last profile until it lands)
   c->len_pending = oo_launch_len_sample(P.desc, n, P.ring_mask, P.ring_cons, c->d_len, ++c->len_seq, s) == 0 &&
                    hipEventRecord(c->len_ev, s) == hipSuccess;
 }
@@ -1759,7 +1786,11 @@ int oo_gpu_rx_submit(oo_gpu_rx_ctx* c, const void* frames, uint64_t frames_bytes
   if (!ok) return -EIO;
   if (n > 0) {
     int rc = prepare(c, st);
-    if (rc == 0) rc = launch(c, s.d_frames, frames_bytes, s.d_desc, n, s.d_out, s.d_ctr, st);
+    if (rc == 0) {
+      c->host_batch = true;
+      rc = launch(c, s.d_frames, frames_bytes, s.d_desc, n, s.d_out, s.d_ctr, st);
+      c->host_batch = false;
+    }
     if (rc) return rc;
     ok = hipMemcpyAsync(s.copy_out ? s.h_out : out, s.d_out, sizeof(oo_gpu_rx_result) * n,
                         hipMemcpyDeviceToHost, st) == hipSuccess;

@@ -314,9 +314,13 @@ def test_incremental_index_falls_back_to_rebuild(cuda):
     for s in (g, o):  # filter-only flush: finds the index off, asks for a rebuild
         assert s.filter_remove(7000, 4, L4A, 6001, None, 0, 17) == 0
     step("update", 0)
-    for s in (g, o):  # the requested rebuild (still off: socket 1's entry is misplaced)
-        assert s.filter_insert(7000, 4, L4A, 6001, None, 0, 17) == 0
+    # no table change: the requested rebuild runs before the next batch all
+    # the same (still off: socket 1's entry is misplaced) -- ADVICE r5
     step("rebuild", 0)
+    step("none", 0)
+    for s in (g, o):  # a filter-only flush finds it off again and asks
+        assert s.filter_insert(7000, 4, L4A, 6001, None, 0, 17) == 0
+    step("update", 0)
     for s in (g, o):  # socket 1's filter re-inserted under its tuple: rebuild, on
         s.filter_remove(1, 4, L4A, 5001, None, 0, 17)
         assert s.filter_insert(1, 4, L4A, 5001, PEER4, 40001, 17) == 0
@@ -324,4 +328,46 @@ def test_incremental_index_falls_back_to_rebuild(cuda):
     for s in (g, o):
         assert s.filter_remove(7000, 4, L4A, 6001, None, 0, 17) == 0
     step("update", 1)
+    g.close()
+
+
+def test_index_rebuilt_after_many_incremental_updates(cuda):
+    """Incremental updates leave KX_DEAD entries behind (a key that lost its
+    last match walks); after 256 of them in a row the next flush rebuilds
+    the index from the tables (oo_gpu_rx.cpp kKxIncMax).  Records
+    equal the oracle's throughout; a batch with no table change flushes
+    nothing."""
+    g, o = _pair()
+    install(g, edge_world())
+    install(o, edge_world())
+    frames = [(_u4(L4A, 5001), 0), (_u4(L4A, 6001), 0)]
+    buf, desc = pack(frames + [(f, i) for f, i in edge_frames()[:30]])
+    for s in (g, o):
+        assert s.sock_set(7000, _sock(17, 6001)) == 0
+    _check(g, o, buf, desc)  # (the socket change: a rebuild)
+    st0 = g.table_stats()
+    for k in range(256):
+        for s in (g, o):
+            if k % 2 == 0:
+                assert s.filter_insert(7000, 4, L4A, 6001, None, 0, 17) == 0
+            else:
+                assert s.filter_remove(7000, 4, L4A, 6001, None, 0, 17) == 0
+        if k % 64 == 63:
+            _check(g, o, buf, desc)
+        else:
+            g.sync()
+    st = g.table_stats()
+    assert st["index_updates"] - st0["index_updates"] == 256, (st0, st)
+    assert st["index_rebuilds"] == st0["index_rebuilds"] and st["index_on"] == 1
+    _check(g, o, buf, desc)  # nothing queued: no flush
+    assert g.table_stats()["index_rebuilds"] == st0["index_rebuilds"]
+    for s in (g, o):
+        assert s.filter_insert(7000, 4, L4A, 6001, None, 0, 17) == 0
+    _check(g, o, buf, desc)
+    st = g.table_stats()
+    assert st["index_rebuilds"] == st0["index_rebuilds"] + 1 and st["index_on"] == 1, (st0, st)
+    for s in (g, o):
+        assert s.filter_remove(7000, 4, L4A, 6001, None, 0, 17) == 0
+    _check(g, o, buf, desc)
+    assert g.table_stats()["index_updates"] == st["index_updates"] + 1  # counting again
     g.close()
