@@ -195,7 +195,8 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
   return s;
 }
 
-#if defined(OO_RX_STAMPS) && !defined(OO_RX_EXPERIMENTS)
+#if (defined(OO_RX_STAMPS) || defined(OO_RX_BOUND_NOLOOK) || defined(OO_RX_BOUND_NOBODY)) && \
+    !defined(OO_RX_EXPERIMENTS)
 #error "OO_RX_STAMPS is a diagnostic build (tools/build_ref.sh sets OO_RX_EXPERIMENTS)"
 #endif
 #ifdef OO_RX_STAMPS
@@ -320,6 +321,14 @@ typedef const __attribute__((address_space(1))) u32x4* g_cu32x4p;
 __device__ __forceinline__ uint32_t gload4(uint64_t a) { return *reinterpret_cast<g_cu32p>(a); }
 __device__ __forceinline__ uint4 gload16(uint64_t a) {
   const u32x4 v = *reinterpret_cast<g_cu32x4p>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// The same load as an instruction the compiler does not track: the caller
+// waits for it with a counted vm_wait before using the value (kx_lookup's
+// first level under window_loop's staging).
+__device__ __forceinline__ uint4 gload16_untracked(uint64_t a) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(a) : "memory");
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -1273,11 +1282,17 @@ __device__ __forceinline__ Match lookup_fsm2(const KParams& P, const ProbeL& t, 
 // the walks would have; false for a lane that must walk: an answer that
 // depends on the packet's interface or VLAN (bind2dev), a UDP key with
 // other than one match, or an index the last table change turned off.
-template <bool ANY6>
+// `issued` runs once, right after the first level's loads are issued and
+// before any of them is waited for (window_loop stages its next tile there,
+// so the two round trips overlap); it issues exactly kIssuedOps
+// vector-memory operations (window_loop's stage: a descriptor line, HC
+// window rows, the claim), or none (the default, [] {}).
+constexpr int kIssuedOps = HC + 2;
+template <bool ANY6, bool STAGE, class F>
 __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool look, bool tcp,
                                           bool any_tcp, uint32_t dport, uint32_t sport,
                                           uint32_t proto, bool o0, bool o1, bool o2, Match& m,
-                                          int& stage, bool& s2) {
+                                          int& stage, bool& s2, F&& issued) {
   const bool six = ANY6 && h.is6;
   uint32_t la[4], sa[4];
 #pragma unroll
@@ -1309,7 +1324,11 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
   // once without a match (its key is not in the index either).
   bool pend[3] = {look && o0, look && o1, look && tcp && o2};
   // One level: every pending key's bucket (entry) loaded, then compared.
-  auto level = [&]() __attribute__((always_inline)) {
+  // (IPv6-capable waves hold 36 VGPRs of buckets: staging under them spills,
+  // so they stage first and overlap nothing)
+  constexpr bool OVERLAP = STAGE && !ANY6;
+  if (!OVERLAP) issued();
+  auto level = [&](bool first) __attribute__((always_inline)) {
     uint4 d[3][3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1317,10 +1336,30 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
         // (a key not looked up reads the region's first bucket: one line
         // for the wave, no branch around the batch)
         const uint64_t a = base + ((uint64_t)(pend[k] ? pos[k] : 0u) << shift);
-        d[k][0] = gload16(a);
-        d[k][1] = gload16(a + 16u);
-        if (ANY6) d[k][2] = gload16(a + 32u);
+        if (OVERLAP && first) {
+          d[k][0] = gload16_untracked(a);
+          d[k][1] = gload16_untracked(a + 16u);
+        } else {
+          d[k][0] = gload16(a);
+          d[k][1] = gload16(a + 16u);
+          if (ANY6) d[k][2] = gload16(a + 32u);
+        }
       }
+    }
+    if (OVERLAP && first) {
+      // The loads are untracked: the compiler sees their values defined at
+      // once, so neither its compares nor any wait of its own move above
+      // `issued`; one counted wait after it covers them -- `issued` issues
+      // exactly kIssuedOps vector-memory operations, all newer.
+      issued();
+      vm_wait<kIssuedOps>();
+      // (the values as written by the loads, from here on)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (k < nk)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            asm volatile("" : "+v"(d[k][j].x), "+v"(d[k][j].y), "+v"(d[k][j].z), "+v"(d[k][j].w));
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1361,7 +1400,7 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
   // The first level is issued at once (a loop head would first wait for
   // every load in flight, the body stream's included); the loop takes the
   // rare keys whose bucket was full.
-  level();
+  level(true);
   bool left = false;
   for (uint32_t it = 1;; ++it) {
     const bool any = pend[0] || pend[1] || pend[2];
@@ -1370,7 +1409,7 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
       left = any;
       break;
     }
-    level();
+    level(false);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(okw));
   const bool f0 = val[0] != 0u, f1 = val[1] != 0u, f2 = tcp && val[2] != 0u;
@@ -1405,10 +1444,13 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
 // its packets mix address families and protocols.
 // LO: the occupancy bitmaps and the hwport bytes are in LDS at lds_occ
 // (OccLds layout, win_kernel).
-template <bool ANY6, bool LO>
+// `issued` (window_loop's next-tile staging) runs exactly once: after the
+// key index's first loads are issued, or -- no lane looking up, or the index
+// off -- before any of the lookup's loads.
+template <bool ANY6, bool LO, bool STAGE, class F>
 __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h, int intf_i,
                                                  uint64_t abase, int span, int shift,
-                                                 uint32_t lds_occ) {
+                                                 uint32_t lds_occ, F&& issued) {
   const int vlan = (int)h.vlan;
   const uint32_t proto = h.proto;
   uint32_t reason = h.reason;
@@ -1418,7 +1460,11 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
   // Lanes that reach the lookups.  The record is assembled after them: its
   // fields come from the headers, which the lookups hold anyway.
   const bool csum_ok = reason == PENDING;
+#ifdef OO_RX_BOUND_NOLOOK  // (a timing bound, wrong records: no lookup at all)
+  const bool look = false;
+#else
   const bool look = csum_ok && h.late == PENDING;
+#endif
   const uint32_t sport = h.sport, dport = h.dport;
   const uint32_t sx = is6 ? h.sa[0] ^ h.sa[1] ^ h.sa[2] ^ h.sa[3] : h.sa[0];  // hash addresses
   const uint32_t dx = is6 ? h.da[0] ^ h.da[1] ^ h.da[2] ^ h.da[3] : h.da[0];
@@ -1486,9 +1532,15 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
     // Lanes that walk the tables: all that look up, less those the key
     // index answers.
     bool walkl = look;
-    if (P.kx4 != nullptr)
-      walkl = look && !kx_lookup<ANY6>(P, h, look, tcp, any_tcp, dport, sport, proto, o0, o1, o2, m,
-                                       stage, s2);
+    if (P.kx4 != nullptr) {
+      // (every lane: `issued` needs the whole wave; a lane that does not
+      // look up loads a dummy bucket and matches nothing)
+      const bool kxa = kx_lookup<ANY6, STAGE>(P, h, look, tcp, any_tcp, dport, sport, proto, o0, o1, o2, m,
+                                       stage, s2, issued);
+      walkl = look && !kxa;
+    } else {
+      issued();
+    }
     Rec rec = {};
     if (walkl && fs < 3) rec = load_rec(P, t, fs == 0 ? h1_0 : fs == 1 ? h1_1 : h1_2, any6);
     if (walkl) {
@@ -1518,6 +1570,8 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
                                                s2);
       DSTAMP(10);
     }
+  } else {
+    issued();
   }
   oo_gpu_rx_result r;
   r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
@@ -1570,13 +1624,21 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
 
 // A wave whose lookups are all IPv4 takes the IPv4-only instance (the
 // IPv6 compares and record halves compiled out).
+// STAGE: `issued` issues kIssuedOps operations (window_loop's staging);
+// otherwise it issues none.
+template <bool LO = false, bool STAGE = false, class F>
+__device__ __forceinline__ Parsed demux_packet(const KParams& P, const Hdr& h, int intf_i,
+                                               uint64_t abase, int span, int shift,
+                                               uint32_t lds_occ, F&& issued) {
+  if (__ballot(h.is6 && h.reason == PENDING && h.late == PENDING) != 0)
+    return demux_packet_t<true, LO, STAGE>(P, h, intf_i, abase, span, shift, lds_occ, issued);
+  return demux_packet_t<false, LO, STAGE>(P, h, intf_i, abase, span, shift, lds_occ, issued);
+}
 template <bool LO = false>
 __device__ __forceinline__ Parsed demux_packet(const KParams& P, const Hdr& h, int intf_i,
                                                uint64_t abase, int span, int shift,
                                                uint32_t lds_occ = 0) {
-  if (__ballot(h.is6 && h.reason == PENDING && h.late == PENDING) != 0)
-    return demux_packet_t<true, LO>(P, h, intf_i, abase, span, shift, lds_occ);
-  return demux_packet_t<false, LO>(P, h, intf_i, abase, span, shift, lds_occ);
+  return demux_packet<LO, false>(P, h, intf_i, abase, span, shift, lds_occ, [] {});
 }
 
 // The verdict a long packet's record waited for: the window part plus the
@@ -2550,7 +2612,11 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // padding rounds read zeros).
     uint32_t myslot;
     const Jobs J = jobs_setup(dv.abase, dv.span, lane, myslot);
+#ifdef OO_RX_BOUND_NOBODY  // (a timing bound, wrong records: no body stream)
+    uint32_t T0 = 0;
+#else
     uint32_t T0 = J.T;
+#endif
     bool ext = E > 0 && T0 > (uint32_t)(R + E);
     uint32_t T = ext ? (T0 - R - E + R - 1) / R * R : (T0 + R - 1) / R * R;
     if (lane == 0) lds_write4(&L.T0, T0);
@@ -2949,47 +3015,46 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
 #define OO_RX_WIN_HDR_AUX 2
 #endif
   bool clean = false;
-  // Prologue: tile t0's descriptors and windows, then t1's descriptors.
+  // Prologue: tile t0's descriptors, then t1's and t0's windows.
   {
     const Unit t0 = unit_of(P, tcur);
     glds<0>(desc_src(P, t0, lane), &L.desc[0][0]);
     vm_wait<0>();
+    glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
     const DescView d0 = desc_view(P, lds_read16(&L.desc[0][lane]), t0, lane);
     stage_window<OO_RX_HDR_AUX>(d0, zero_line(P, t0, lane), L.hdr, lane);
     clean = __ballot(d0.span > 64) == 0;
-    glds<0>(desc_src(P, unit_of(P, tnext), lane), &L.desc[1][0]);
   }
 
   uint32_t b = 0;
   for (uint32_t it_ = 0; tcur < P.ntiles; b ^= 1u, ++it_) {
     const Unit tile = unit_of(P, tcur);
-    // This tile's windows (and its descriptors, older): newer are the next
-    // tile's descriptor line and, after the first tile, the claim and the
-    // previous tile's record stores.
-    if (it_ == 0) vm_wait<1>();
-    else vm_wait<2 + NST>();
+    // This tile's windows, and the next tile's descriptors (issued before
+    // them): newer are, after the first tile, the claim and the previous
+    // tile's record stores.
+    if (it_ == 0) vm_wait<0>();
+    else vm_wait<1 + NST>();
+    // The claim made at the last tile's staging: the tile after the next
+    // one.  (Read here, not in the staging below, where the compiler's wait
+    // for it would also wait for the key index loads.)
+    if (it_ != 0) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+      tnext2 = P.dyn ? 3u * W + g + c : tnext2 + W;
+    }
     const DescView dv = desc_view(P, lds_read16(&L.desc[b][lane]), tile, lane);
     // (the window's cell addresses recomputed per tile: hoisted, eight
     // loop-long registers would spill)
     uint32_t wl = lane;
     asm volatile("" : "+v"(wl));
     const Hdr h = parse_headers(window_of(L.hdr, wl), dv.shift, dv.len, dv.abase);
-    // ---- lookups and the record: before the next tile's staging, so the
-    // demux's waits do not also wait for those loads (config 3 -0.3 to -2 %,
-    // profiles/r04/ab_win_demux_first.log).
-    Parsed ps = demux_packet<true>(P, h, dv.intf_i, dv.abase, dv.span, dv.shift, lds_occ);
-
-    // ---- stage the next tile: its windows into the rows the parse has
-    // read (its descriptor line: newer are the claim and the record stores),
-    // the descriptors of the tile after it, the claim of the tile after that.
-    if (it_ != 0) {
-      const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
-      tnext2 = P.dyn ? 3u * W + g + c : tnext2 + W;
-      vm_wait<1 + NST>();
-    } else {
-      vm_wait<0>();
-    }
-    {
+    // ---- lookups and the record.  The next tile is staged inside the
+    // demux, as soon as the key index's loads are issued and before they
+    // are waited for, so the lookup's round trip and the staging's overlap
+    // (DESIGN.md §5 round 6): the descriptors of the tile after it into the
+    // buffer this tile's came in (read above), its windows into the rows
+    // the parse has read, the claim of the tile after that.
+    auto stage = [&]() {
+      glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
       const Unit nt = unit_of(P, tnext);
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the parse's LDS reads are done
@@ -3000,9 +3065,9 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       else
         stage_window<OO_RX_HDR_AUX>(dn, zero_line(P, nt, lane), L.hdr, lane, false);
       clean = short4;
-    }
-    glds<0>(desc_src(P, unit_of(P, tnext2), lane), &L.desc[b][0]);
-    claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
+      claim_tile(P.claim + 32u * g, P.ngroups, lane, got);
+    };
+    Parsed ps = demux_packet<true, true>(P, h, dv.intf_i, dv.abase, dv.span, dv.shift, lds_occ, stage);
 
     const uint32_t reason = ps.r.reason;
     store_records(P, tile, ps.r, lane);
