@@ -195,8 +195,8 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
   return s;
 }
 
-#if (defined(OO_RX_STAMPS) || defined(OO_RX_BOUND_NOLOOK) || defined(OO_RX_BOUND_NOBODY)) && \
-    !defined(OO_RX_EXPERIMENTS)
+#if (defined(OO_RX_STAMPS) || defined(OO_RX_BOUND_NOLOOK) || defined(OO_RX_BOUND_NOBODY) || \
+     defined(OO_RX_BOUND_KXLINE) || defined(OO_RX_BOUND_KX1)) && !defined(OO_RX_EXPERIMENTS)
 #error "OO_RX_STAMPS is a diagnostic build (tools/build_ref.sh sets OO_RX_EXPERIMENTS)"
 #endif
 #ifdef OO_RX_STAMPS
@@ -1335,10 +1335,18 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
       if (k < nk) {
         // (a key not looked up reads the region's first bucket: one line
         // for the wave, no branch around the batch)
+#ifdef OO_RX_BOUND_KXLINE  // (timing bound, wrong records: every lane loads one bucket)
+        const uint64_t a = base;
+#else
         const uint64_t a = base + ((uint64_t)(pend[k] ? pos[k] : 0u) << shift);
+#endif
         if (OVERLAP && first) {
           d[k][0] = gload16_untracked(a);
+#ifdef OO_RX_BOUND_KX1  // (timing bound, wrong records: the bucket's first entry only)
+          d[k][1] = make_uint4(0u, 0u, 0u, 0u);
+#else
           d[k][1] = gload16_untracked(a + 16u);
+#endif
         } else {
           d[k][0] = gload16(a);
           d[k][1] = gload16(a + 16u);
@@ -2433,22 +2441,6 @@ constexpr int NST = 2;
 constexpr int E = OO_RX_EXTRA;
 static_assert(E % 2 == 0 && E <= HC, "extra rounds live in the header rows");
 
-// The deep ring (OO_RX_DEEP, rx_kernel only): once the parse has read the
-// header rows, the R ring rows and the HC header rows are one ring of
-// S = R + HC slots for the whole body, not only for E extra rounds -- round k
-// in row (k + HC) mod S -- and each header row takes its window of the next
-// tile when its last round of this tile has been consumed (a row no round
-// reaches takes it right after the demux).  Every tile keeps S rounds in
-// flight through its body where the plain loop keeps R after its first
-// R + E, at the price of the next tile's windows landing during this tile's
-// last rounds instead of during its whole body.
-// The waits are counted from each slot's issue index (a lane of one VGPR),
-// so they hold for any mix of refills and window rows.
-#ifndef OO_RX_DEEP
-#define OO_RX_DEEP 0
-#endif
-constexpr int S_DEEP = R + HC;
-
 struct WaveLds {
   uint4 hdr[HC][64];            // header windows (stage_window)
   uint4 ring[R][64];            // body ring: slot = one round of the eight groups
@@ -2641,31 +2633,8 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // and after the demux: issued before it they are older than its loads,
     // and every demux wait would wait for them too (configs 2/4/5 -1.7 /
     // -0.5 / -0.7 %, profiles/r04/ab_extra_after_demux.log).
-    // The deep ring: header row h's window of the next tile (packet p's
-    // cell c for lane (p & 7, c), as stage_window lays it out), its
-    // descriptor read from LDS by the lane itself.
-    constexpr bool DEEP = OO_RX_DEEP && !TX && E == HC;
-    auto window_row = [&](uint32_t h) {
-      const Unit nt = unit_of(P, tnext);
-      const uint32_t p = h * 8u + (lane >> 3);
-      const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][p]), nt, p);
-      const uint32_t c = ((lane & 7u) + p) & 7u;
-      const int nwin = (dn.span + 15) >> 4;
-      glds<OO_RX_HDR_AUX>((int)c < nwin ? dn.abase + (uint64_t)c * 16 : zero_line(P, nt, lane),
-                          &L.hdr[h][0]);
-    };
     auto issue_extra = [&]() {
-      if constexpr (DEEP) {
-        // Rounds R..S-1 into the header rows, in order; a row no round of
-        // this tile reaches takes its next-tile window now.
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint32_t t0 = sreg(lds_read4(&L.T0));
-#pragma unroll
-        for (int u = 0; u < HC; ++u) {
-          if ((uint32_t)(R + u) < t0) issue_round(ci, J, zero, &L.hdr[u][0], lane);
-          else window_row((uint32_t)u);
-        }
-      } else if (ext) {
+      if (ext) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int u = 0; u < E; ++u) issue_round(ci, J, zero, &L.hdr[u][0], lane);
@@ -2717,7 +2686,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       const DescView dn = desc_view(P, lds_read16(&L.desc[b ^ 1u][lane]), nt, lane);
       stage_window(dn, zero_line(P, nt, lane), L.hdr, lane);
     };
-    if (!DEEP && !ext) stage_next();
+    if (!ext) stage_next();
 
     claim_tile(P.claim + sreg(lds_read4(&L.gofs)), P.ngroups, lane, got);  // tile i + 3
 
@@ -2731,47 +2700,10 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       cc.bs = 0;
     }
 
-    if constexpr (DEEP) {
-      // Issue indices since the tile's start: slot s (round s's, or for a
-      // header row no round reached, its window) was op s + 1; then the
-      // descriptor line and the claim.  Round k's slot is k mod S; waiting
-      // for it leaves the ops issued after it outstanding.
-      constexpr uint32_t S = (uint32_t)S_DEEP;
-      uint32_t rs = lane + 1u;  // lane s: issue index of slot s's op
-      uint32_t q = S + 2u;      // ops issued so far
-      uint32_t s0 = 0;          // slot of round k
-      for (uint32_t k = 0; k < T0; k += 2, s0 = s0 + 2u == S ? 0u : s0 + 2u) {
-        const uint32_t s1 = s0 + 1u;  // (S even: a pair never wraps)
-        const uint32_t idx = (uint32_t)__builtin_amdgcn_readlane((int)rs, (int)(k + 1u < T0 ? s1 : s0));
-        vm_wait_n((int)(q - idx));
-        const uint32_t r0 = s0 < (uint32_t)R ? s0 + HC : s0 - R;
-        const uint32_t r1 = s1 < (uint32_t)R ? s1 + HC : s1 - R;
-        uint4 v0, v1;  // (round T0, past the end when T0 is odd: weighed 0)
-        lds_read16x2(&L.hdr[r0][lane], &L.hdr[r1][lane], v0, v1);
-        consume_round(cc, J, v0, lane);
-        consume_round(cc, J, v1, lane);
-        // The two slots: their next round, else (a header row) the next
-        // tile's window, else nothing.
-#pragma unroll
-        for (uint32_t d = 0; d < 2u; ++d) {
-          const uint32_t j = k + d, s = s0 + d, row = d ? r1 : r0;
-          if (j >= T0) continue;
-          if (j + S < T0) {
-            issue_round(ci, J, zero, &L.hdr[row][0], lane);
-            rs = lane == s ? q + 1u : rs;
-            ++q;
-          } else if (s >= (uint32_t)R) {
-            window_row(row);
-            ++q;
-          }
-        }
-      }
-    }
-
     // ---- body stream, two pieces per step.  Each wait counts the
     // operations issued after the awaited pair (the demux loads excepted:
     // the demux waited for its last one, and with it for everything older).
-    if (!DEEP && ext) {
+    if (ext) {
       // Ring rounds 0..R-1, refilled with R+E..R+E+R-1: newer than the
       // pair, the rest of the ring, the E header-row rounds, the descriptor
       // line and the claim, and the refills so far -- R + E in all.
@@ -2801,7 +2733,7 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
     // rest of the ring, plus in the first turn the staging operations issued
     // since the ring was filled (NHS, or HC after an ext prefix); none past T.
     const int nhs = ext ? HC : NHS;
-    for (uint32_t k0 = 0; k0 < (DEEP ? 0u : T); k0 += R) {
+    for (uint32_t k0 = 0; k0 < T; k0 += R) {
       const bool first = k0 == 0, last = k0 + R == T;
 #pragma unroll
       for (int u = 0; u < R; u += 2) {

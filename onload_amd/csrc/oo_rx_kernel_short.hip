@@ -11,7 +11,4 @@
 #undef OO_RX_GSEQ
 #define OO_RX_GSEQ 1
 #define OO_RX_SHORT 1
-#if defined(OO_RX_SHORT_DEEP) && !defined(OO_RX_DEEP)
-#define OO_RX_DEEP OO_RX_SHORT_DEEP
-#endif
 #include "oo_rx_kernel.hip"
