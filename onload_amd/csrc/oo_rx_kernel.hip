@@ -196,7 +196,8 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
 }
 
 #if (defined(OO_RX_STAMPS) || defined(OO_RX_BOUND_NOLOOK) || defined(OO_RX_BOUND_NOBODY) || \
-     defined(OO_RX_BOUND_KXLINE) || defined(OO_RX_BOUND_KX1)) && !defined(OO_RX_EXPERIMENTS)
+     defined(OO_RX_BOUND_KXLINE) || defined(OO_RX_BOUND_KX1) || defined(OO_RX_BOUND_NOGENSUM)) && \
+    !defined(OO_RX_EXPERIMENTS)
 #error "OO_RX_STAMPS is a diagnostic build (tools/build_ref.sh sets OO_RX_EXPERIMENTS)"
 #endif
 #ifdef OO_RX_STAMPS
@@ -714,7 +715,12 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
   const int cut = E4 > HB ? off0 : E4;
   const int lo4 = min(S4, cut), hi4 = max(S4, cut);
   uint32_t s3 = 0, s4 = 0;
+#ifdef OO_RX_BOUND_NOGENSUM  // (timing bound, wrong records: no window sums in the general walk;
+  s3 = 0xffffu;              //  the IPv4 check passes, so the same packets reach the lookups
+  if (false) {               //  and the same bodies stream)
+#else
   if (need_ip || need_l4) {
+#endif
 #pragma unroll
     for (int k = 0; k < HC; ++k) {
       const uint4 v = *reinterpret_cast<const uint4*>(W.cell(k));
