@@ -2974,7 +2974,9 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     else vm_wait<1 + NST>();
     // The claim made at the last tile's staging: the tile after the next
     // one.  (Read here, not in the staging below, where the compiler's wait
-    // for it would also wait for the key index loads.)
+    // for it would also wait for the key index loads.  Claiming at the
+    // tile's start instead, before those loads, measured 4 % slower on
+    // config 3: profiles/r06/ab_win_stage_overlap_c3_c4.log.)
     if (it_ != 0) {
       const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
       tnext2 = P.dyn ? 3u * W + g + c : tnext2 + W;

@@ -181,3 +181,31 @@ def test_split_store_counts(asm):
     assert not re.findall(r"global_store_(byte|short)", w)
     for k in (WIN, BODY):
         assert not re.findall(r"flat_store|flat_load|flat_atomic", _body(text, k)), k
+
+
+def test_win_kernel_counted_wait_after_staging(asm):
+    """window_loop stages the next tile inside the demux (oo_rx_kernel.hip
+    kx_lookup, `issued`): the key index's first-level loads are untracked and
+    one counted `s_waitcnt vmcnt(HC + 2)` (the inline-asm vm_wait) after the
+    staging covers them.  That holds only if every path from those loads to
+    the wait issues exactly HC + 2 = 10 vector-memory operations -- the
+    descriptor line, one of the two staging forms (all rows, or masked rows:
+    eight LDS-DMA rows each), the claim.  (A compiler wait in between only
+    makes the counted one redundant.)"""
+    text, _ = asm
+    win = _body(text, WIN).splitlines()
+    sites = [i for i, l in enumerate(win)
+             if re.search(r"s_waitcnt vmcnt\(10\)", l) and "ASMSTART" in win[i - 1]]
+    assert sites, "no counted wait after the staging"
+    for w in sites:
+        i, lds, other = w - 2, 0, []
+        while not re.match(r"^\s*global_load_dwordx4 v\[\d+:\d+\], v\[\d+:\d+\], off$", win[i]):
+            if "global_load_lds" in win[i]:
+                lds += 1
+            elif re.match(r"^\s*(global_|buffer_|scratch_|flat_)", win[i]):
+                other.append(win[i].split()[0])
+            i -= 1
+            assert i >= 0, "no untracked load before the counted wait"
+        # the descriptor line and the two staging forms laid out one after
+        # the other, then the claim
+        assert lds == 1 + 8 + 8 and other == ["global_atomic_add"], (w, lds, other)
