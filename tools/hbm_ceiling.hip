@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -79,6 +80,44 @@ static float time_it(K kern, int grid, const u32x4* a, size_t n16, uint32_t* o) 
   return best;
 }
 
+// "ramp" mode (argv[2]): the stream ceiling launch by launch from a cold
+// start, the way bench.py's driver window sees it -- after an idle second,
+// `launches` back-to-back launches of the LDS-DMA stream (nt, 8 waves per
+// CU), each timed by its own event pair; prints the per-launch GB/s and the
+// means over launches 6-25 (bench.py's --warmup 5 --steps 20 window) and
+// 26-225 (its `steady` side measurement).
+static int ramp(const u32x4* a, size_t bytes, uint32_t* o, int cu, int launches) {
+  const size_t n16 = bytes / 16;
+  hipEvent_t* e = (hipEvent_t*)malloc(sizeof(hipEvent_t) * (launches + 1));
+  for (int i = 0; i <= launches; ++i) (void)hipEventCreate(&e[i]);
+  (void)hipDeviceSynchronize();
+  const hipError_t s = hipDeviceSynchronize();
+  if (s != hipSuccess) return 1;
+  // (idle: the clocks drop as they do between bench.py's setup and its warm-up)
+  struct timespec ts = {1, 0};
+  nanosleep(&ts, nullptr);
+  (void)hipEventRecord(e[0], 0);
+  for (int i = 0; i < launches; ++i) {
+    hipLaunchKernelGGL(read_lds<2>, dim3(cu * 8), dim3(256), 0, 0, a, n16, o);
+    (void)hipEventRecord(e[i + 1], 0);
+  }
+  (void)hipEventSynchronize(e[launches]);
+  double w = 0, sdy = 0;
+  int nw = 0, ns = 0;
+  printf("{\"bytes\":%zu,\"gbps\":[", bytes);
+  for (int i = 0; i < launches; ++i) {
+    float ms;
+    (void)hipEventElapsedTime(&ms, e[i], e[i + 1]);
+    const double g = bytes / (ms * 1e-3) / 1e9;
+    printf("%s%.1f", i ? "," : "", g);
+    if (i >= 5 && i < 25) { w += ms; ++nw; }
+    if (i >= 25) { sdy += ms; ++ns; }
+  }
+  printf("],\"window_6_25_GBps\":%.1f,\"steady_26_GBps\":%.1f}\n",
+         nw ? bytes / (w / nw * 1e-3) / 1e9 : 0.0, ns ? bytes / (sdy / ns * 1e-3) / 1e9 : 0.0);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const size_t bytes = (argc > 1 ? strtoull(argv[1], 0, 0) : (size_t)2 << 30);
   const size_t n16 = bytes / 16;
@@ -89,6 +128,7 @@ int main(int argc, char** argv) {
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
   const int cu = prop.multiProcessorCount;
+  if (argc > 2 && argv[2][0] == 'r') return ramp(a, bytes, o, cu, argc > 3 ? atoi(argv[3]) : 225);
   for (int m : {4, 8, 16, 32}) {
     const int g = cu * m;
     const float t1 = time_it(read_reg<true>, g, a, n16, o);
