@@ -226,12 +226,23 @@ __device__ uint64_t* dstamp_slot(uint64_t* p = nullptr, bool set = false) {
     uint64_t* dp_ = dstamp_slot();                                                    \
     if (dp_ != nullptr && __builtin_amdgcn_mbcnt_lo(~0u, 0u) == 0) dp_[(ph)] = (v);   \
   } while (0)
+#define DSTAMPA(ph)                                                                   \
+  do {                                                                                \
+    uint64_t* dp_ = dstamp_slot();                                                    \
+    const uint64_t ex_ = __ballot(1);                                                 \
+    if (dp_ != nullptr && __builtin_amdgcn_mbcnt_hi((uint32_t)(ex_ >> 32),            \
+                            __builtin_amdgcn_mbcnt_lo((uint32_t)ex_, 0u)) == 0)      \
+      dp_[(ph)] = __builtin_amdgcn_s_memrealtime();                                   \
+  } while (0)
 #else
 #define DSTAMP(ph) \
   do {             \
   } while (0)
 #define DSTAMPV(ph, v) \
   do {                 \
+  } while (0)
+#define DSTAMPA(ph) \
+  do {              \
   } while (0)
 #define STAMP(ph, val) \
   do {                 \
@@ -600,6 +611,338 @@ struct Win {
   }
 };
 
+// The staged window of this lane's packet in registers (one LDS wait).
+__device__ __forceinline__ void read_cells(const Win& W, uint4 (&c)[HC]) {
+  static_assert(HC == 8, "eight window cells");
+  uint32_t a[HC];
+#pragma unroll
+  for (int k = 0; k < HC; ++k) a[k] = (uint32_t)(uintptr_t)(lptr)(W.cell(k));
+  asm volatile(
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\t"
+      "ds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\t"
+      "ds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\t"
+      "ds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3]), "=&v"(c[4]), "=&v"(c[5]),
+        "=&v"(c[6]), "=&v"(c[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
+      : "memory");
+}
+
+// K aligned 4-byte LDS reads in one batch with one wait.
+template <int K>
+__device__ __forceinline__ void lds_read_b32s(const uint32_t (&a)[K], uint32_t (&d)[K]);
+template <>
+__device__ __forceinline__ void lds_read_b32s<7>(const uint32_t (&a)[7], uint32_t (&d)[7]) {
+  asm volatile("ds_read_b32 %0, %7\n\tds_read_b32 %1, %8\n\tds_read_b32 %2, %9\n\tds_read_b32 %3, %10\n\tds_read_b32 %4, %11\n\tds_read_b32 %5, %12\n\tds_read_b32 %6, %13\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6])
+               : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6])
+               : "memory");
+}
+template <>
+__device__ __forceinline__ void lds_read_b32s<11>(const uint32_t (&a)[11], uint32_t (&d)[11]) {
+  asm volatile("ds_read_b32 %0, %11\n\tds_read_b32 %1, %12\n\tds_read_b32 %2, %13\n\tds_read_b32 %3, %14\n\tds_read_b32 %4, %15\n\tds_read_b32 %5, %16\n\tds_read_b32 %6, %17\n\tds_read_b32 %7, %18\n\tds_read_b32 %8, %19\n\tds_read_b32 %9, %20\n\tds_read_b32 %10, %21\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]), "=&v"(d[8]), "=&v"(d[9]), "=&v"(d[10])
+               : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]), "v"(a[9]), "v"(a[10])
+               : "memory");
+}
+template <>
+__device__ __forceinline__ void lds_read_b32s<13>(const uint32_t (&a)[13], uint32_t (&d)[13]) {
+  asm volatile("ds_read_b32 %0, %13\n\tds_read_b32 %1, %14\n\tds_read_b32 %2, %15\n\tds_read_b32 %3, %16\n\tds_read_b32 %4, %17\n\tds_read_b32 %5, %18\n\tds_read_b32 %6, %19\n\tds_read_b32 %7, %20\n\tds_read_b32 %8, %21\n\tds_read_b32 %9, %22\n\tds_read_b32 %10, %23\n\tds_read_b32 %11, %24\n\tds_read_b32 %12, %25\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]), "=&v"(d[8]), "=&v"(d[9]), "=&v"(d[10]), "=&v"(d[11]), "=&v"(d[12])
+               : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12])
+               : "memory");
+}
+
+// Frame bytes [j0, j0 + 4 (K - 1)) of this lane's window (frame byte j at
+// window position shift + j) as K - 1 little-endian words: K aligned reads
+// from window position (shift + j0) & ~3 on, one batch, realigned (a word
+// never straddles a cell; a position past the window wraps inside the row
+// and is only ever read for bytes nothing uses).
+template <int K>
+__device__ __forceinline__ void window_run(const Win& W, int shift, int j0, uint32_t (&o)[K - 1]) {
+  const uint32_t p = (uint32_t)(shift + j0);
+  const uint32_t row = (uint32_t)(uintptr_t)(lptr)(W.row);
+  uint32_t a[K], d[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const uint32_t q = (p & ~3u) + 4u * (uint32_t)i;
+    a[i] = row + ((((q >> 4) + W.rot) & 7u) << 4) + (q & 12u);
+  }
+  lds_read_b32s<K>(a, d);
+#pragma unroll
+  for (int i = 0; i < K - 1; ++i) o[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], p & 3u);
+}
+
+// (A per-lane select by lane mask: the compiler turns a select between
+// neighbouring array elements into an indexed access through scratch.)
+__device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t if0, uint32_t if1) {
+  uint32_t r;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
+  return r;
+}
+
+// Bytes r, r + 1 of the option words O (r < 40) in the low half.
+__device__ __forceinline__ uint32_t opt_pair(const uint32_t (&O)[10], int r) {
+  const uint32_t i = (uint32_t)r >> 2;
+  uint32_t lo = O[0], hi = O[1];
+#pragma unroll
+  for (int k = 1; k < 10; ++k) {
+    const uint64_t m = __ballot(i == (uint32_t)k);
+    lo = vsel(m, lo, O[k]);
+    hi = vsel(m, hi, k + 1 < 10 ? O[k + 1] : 0u);
+  }
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)r & 3u);
+}
+
+// Bit i: option byte i is not IPOPT_NOP (bytes 0..39).
+__device__ __forceinline__ uint64_t opt_not_nop(const uint32_t (&O)[10]) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const uint32_t x = O[k] ^ 0x01010101u;
+    // bit 7 of each byte: the byte is non-zero; gathered to bits 28..31
+    const uint32_t y = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+    m |= (uint64_t)((y * 0x00204081u) >> 28) << (4 * k);
+  }
+  return m;
+}
+
+#ifndef OO_RX_GEN_RUNS  // the general header walk by word runs (parse_general_runs)
+#define OO_RX_GEN_RUNS 1
+#endif
+// The general header walk by runs (OO_RX_GEN_RUNS): the same decisions as
+// parse_general below in fewer instructions -- config 4's win_kernel issues
+// instructions most of the time, and its walk was 13 of 22 us per tile
+// (stamps).  Fields come from a few word runs of the window, each one batch
+// of LDS reads (frame bytes 12..63: Ethernet type, VLAN tag and the L3
+// header at either place; the L4 header's first 24 bytes; the IPv4
+// options); the IPv4 header sum from those words (frame-aligned pairs: the
+// folded sum is the window-aligned one byte-swapped, and 0xffff either
+// way, RFC 1071); the option walk steps from one non-NOP byte to the next.
+__device__ __forceinline__ Hdr parse_general_runs(const Win& W, int shift, int len, int off0) {
+  // Frame bytes [12, 60).  Only bytes 12..15 can lie past the frame and
+  // still be used (the VLAN tag is recorded for any length): masked.
+  uint32_t F[12];
+  window_run<13>(W, shift, 12, F);
+  {
+    const int nv = len - 12;
+    F[0] &= nv >= 4 ? 0xffffffffu : nv <= 0 ? 0u : (1u << (8 * nv)) - 1u;
+  }
+  auto bF = [&](int i) -> uint32_t { return (F[i >> 2] >> (8 * (i & 3))) & 0xffu; };  // byte 12 + i
+  auto BE16F = [&](int i) -> uint32_t { return (bF(i) << 8) | bF(i + 1); };
+
+  Hdr h;
+  h.flags = 0;
+  h.late = PENDING;
+  const bool vl = BE16F(0) == 0x8100u;  // ci_parse_rx_vlan (netif_event.c:116-132)
+  const int pre_l3 = vl ? 18 : 14;
+  h.vlan = vl ? BE16F(2) & 0xfffu : 0u;
+  if (vl) h.flags |= OO_RX_F_VLAN;
+  // The L3 header's first 40 bytes: L[k] = frame bytes l3 + 4k .. l3 + 4k + 3.
+  uint32_t L[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k)
+    L[k] = vl ? __builtin_amdgcn_alignbyte(F[k + 2], F[k + 1], 2u)
+              : __builtin_amdgcn_alignbyte(F[k + 1], F[k], 2u);
+  auto bL = [&](int i) -> uint32_t { return (L[i >> 2] >> (8 * (i & 3))) & 0xffu; };
+  auto BE16L = [&](int i) -> uint32_t { return (bL(i) << 8) | bL(i + 1); };
+  auto N16L = [&](int i) -> uint32_t { return (L[i >> 2] >> (8 * (i & 3))) & 0xffffu; };  // i even
+
+  const int l3 = pre_l3;
+  uint32_t reason = PENDING;
+  bool is6 = false, l3ok = false;
+  int ip_len = 0, ihl4 = 0, ip_paylen = 0, l4 = 0;
+  uint32_t proto = 0;
+  if (len < pre_l3 + 20) {  // netif_event.c:1030
+    reason = OO_RX_R_SHORT_L2;
+  } else {
+    const uint32_t et = vl ? BE16F(4) : BE16F(0);
+    if (et == 0x0800u) {  // :1038-1058
+      l3ok = true;
+      ip_len = (int)BE16L(2);
+      ihl4 = (int)(bL(0) & 0xfu) * 4;
+      ip_paylen = ip_len - ihl4;
+      proto = bL(9);
+      if (ip_paylen <= 0 || len < pre_l3 + ip_len) reason = OO_RX_R_IP4_LEN;
+      l4 = l3 + ihl4;
+    } else if (et == 0x86ddu) {  // :1060-1076
+      l3ok = true;
+      is6 = true;
+      h.flags |= OO_RX_F_IP6;
+      ip_paylen = (int)BE16L(4);
+      proto = bL(6);
+      if (ip_paylen <= 0 || len < pre_l3 + 40 + ip_paylen) reason = OO_RX_R_IP6_LEN;
+      l4 = l3 + 40;
+    } else {
+      reason = OO_RX_R_NOT_IP;  // :1078
+    }
+  }
+  DSTAMPA(9);
+
+  // Frame bytes [l4, l4 + 24): every field read from them is inside the
+  // frame whenever it is used (the gates come first).
+  uint32_t G[6];
+  window_run<7>(W, shift, l4, G);
+  auto bG = [&](int i) -> uint32_t { return (G[i >> 2] >> (8 * (i & 3))) & 0xffu; };
+  auto N16G = [&](int i) -> uint32_t { return (G[i >> 2] >> (8 * (i & 3))) & 0xffffu; };  // i even
+  // The IPv4 options, bytes [l3 + 20, l3 + 60), when some lane has any.
+  const int nopt = l3ok && !is6 && ihl4 > 20 ? (ihl4 - 20) >> 2 : 0;  // option words
+  uint32_t O[10];
+  if (__ballot(nopt != 0) != 0) {
+    window_run<11>(W, shift, l3 + 20, O);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) O[k] = 0u;
+  }
+
+  // L4 gates (netif_event.c:1084-1127) -> which region to sum.
+  uint32_t l4_gate = PENDING;
+  bool need_l4 = false;
+  int l4_len = 0;
+  uint32_t pseudo = 0;
+  if (reason == PENDING) {
+    if (proto == 6u) {
+      const int hlen = (int)((bG(12) & 0xf0u) >> 2);
+      if (ip_paylen < 20) l4_gate = OO_RX_R_TCP_SHORT;
+      else if (hlen < 20 || ip_paylen < hlen) l4_gate = OO_RX_R_TCP_CSUM;
+      else { need_l4 = true; l4_len = ip_paylen; }
+    } else if (proto == 17u) {
+      const uint32_t udp_len = swap16(N16G(4));
+      if (ip_paylen < 8) l4_gate = OO_RX_R_UDP_SHORT;
+      else if (udp_len < 8u || udp_len > (uint32_t)ip_paylen) l4_gate = OO_RX_R_UDP_CSUM;
+      else if (!(N16G(6) == 0u && !is6)) { need_l4 = true; l4_len = (int)udp_len; }
+    } else {
+      l4_gate = OO_RX_R_PROTO_OTHER;
+    }
+    if (need_l4) {
+      // Pseudo-header words (checksum.c:215-223, 304-305, 334-335).
+      if (is6) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int k = 2; k < 10; ++k) a = dot(L[k], 0x00010001u, a);
+        pseudo = a + (proto == 6u ? N16L(4) + 0x0600u : N16G(4) + 0x1100u);
+      } else {
+        pseudo = dot(L[4], 0x00010001u, dot(L[3], 0x00010001u, 0u));
+        if (proto == 6u) {
+          const uint32_t pl = (uint32_t)ip_paylen & 0xffffu;
+          pseudo += 0x0600u + (((pl & 0xffu) << 8) | (pl >> 8));
+        } else {
+          pseudo += 0x1100u + N16G(4);
+        }
+      }
+    }
+  }
+  DSTAMPA(10);
+
+  // The IPv4 header's word sum (its 20 bytes and the option words), and the
+  // L4 region's window part over the cells: [S4,E4) when it ends inside the
+  // window, else [S4,off0) (signed: the body stream starts at window byte
+  // off0, which may lie before S4).
+  const bool need_ip = reason == PENDING && !is6;
+  const int S4 = shift + l4, E4 = need_l4 ? shift + l4 + l4_len : S4;
+  const int cut = E4 > HB ? off0 : E4;
+  const int lo4 = min(S4, cut), hi4 = max(S4, cut);
+  uint32_t s3 = 0, s4 = 0;
+  if (need_ip) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) s3 = dot(L[k], 4 * k < ihl4 ? 0x00010001u : 0u, s3);  // (IHL < 5 too)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) s3 = dot(O[k], k < nopt ? 0x00010001u : 0u, s3);
+  }
+  if (need_l4) {
+    uint4 c[HC];  // (read again: held across the walk they cost a spill)
+    read_cells(W, c);
+#pragma unroll
+    for (int k = 0; k < HC; ++k)
+      if (k * 16 < hi4) s4 += chunk_sum(c[k], k * 16, lo4, hi4);
+    if (cut < S4) s4 = 0u - s4;
+  }
+  if (reason == PENDING && need_ip) {
+    // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
+    if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
+  }
+  if (reason == PENDING && l4_gate != PENDING) reason = l4_gate;
+
+  // L4 verdict now when the region ends inside the window; otherwise it
+  // waits for the body stream and the record is speculative.
+  const bool longl4 = reason == PENDING && need_l4 && E4 > HB;
+  if (reason == PENDING && need_l4 && !longl4) {
+    uint32_t f = fold16(s4);
+    if (shift & 1) f = swap16(f);  // RFC 1071 byte-order swap
+    if (fold16(f + pseudo) != 0xffffu)
+      reason = proto == 6u ? OO_RX_R_TCP_CSUM : OO_RX_R_UDP_CSUM;
+  }
+
+  // The TCP timestamp-option fast layout (tcp_rx.c:4537-4543).
+  if (reason == PENDING && proto == 6u && bG(12) == 0x80u && G[5] == 0x0a080101u)
+    h.flags |= OO_RX_F_TSO;
+  DSTAMPA(11);
+  h.reason = reason;
+  h.proto = proto;
+  h.ip_paylen = (uint32_t)ip_paylen;
+  h.l4 = (uint32_t)l4;
+  h.l3ok = l3ok;
+  h.is6 = is6;
+  h.longl4 = longl4;
+  h.s4 = s4;
+  h.pseudo = pseudo;
+  h.E4 = E4;
+  h.sport = h.dport = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h.sa[i] = h.da[i] = 0;
+  if (reason == PENDING) {
+    h.sport = N16G(0);
+    h.dport = N16G(2);
+    if (is6) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        h.sa[i] = L[2 + i];
+        h.da[i] = L[6 + i];
+      }
+    } else {
+      h.sa[0] = L[3];
+      h.da[0] = L[4];
+      const uint32_t frag = BE16L(6);
+      uint32_t late = PENDING;
+      DSTAMPA(12);
+      if ((frag & 0x3fffu) != 0 || ip_len > len - pre_l3) {
+        late = OO_RX_R_IP4_FRAG;  // netif_event.c:293-295
+      } else if (ihl4 > 20) {
+        // ci_ip_options_parse (netif_event.c:135-185), signed-char lengths:
+        // from one non-NOP byte to the next (a NOP only ever advances one
+        // byte); a step past the options' end, or onto IPOPT_EOL, ends it.
+        const uint64_t nn = opt_not_nop(O);
+        const int end = ihl4 - 20;
+        int o = 0;
+        bool err = false;
+        for (;;) {
+          const uint64_t rest = nn >> o;
+          o += rest != 0 ? (int)__builtin_ctzll(rest) : 64;
+          if (o >= end) break;
+          const uint32_t b2 = opt_pair(O, o);
+          const uint32_t kind = b2 & 0xffu;
+          if (kind == 0u) break;  // IPOPT_EOL
+          if (kind == 7u || kind == 68u || kind == 130u || kind == 136u) {
+            const int l = (int)(int8_t)(uint8_t)(b2 >> 8);
+            if (l < 4 || l > end - o) { err = true; break; }
+            o += l;
+            if (o >= end) break;
+          } else {
+            err = true;
+            break;
+          }
+        }
+        if (err) late = OO_RX_R_IP4_OPTS_BAD;
+      }
+      if (late == PENDING && proto == 6u && frag != 0x4000u && frag != 0u)
+        late = OO_RX_R_TCP_SCATTERED;  // tcp_rx.c:4696-4699
+      h.late = late;
+    }
+  }
+  return h;
+}
+
 // The general header walk (any VLAN / IP version / IHL / options / alignment)
 // over the staged window: handle_rx_csum_bad (netif_event.c:1024-1127) and
 // the IPv4 checks of handle_rx_pkt (:293-303, tcp_rx.c:4696-4699).  Window
@@ -666,6 +1009,7 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
       reason = OO_RX_R_NOT_IP;  // :1078
     }
   }
+  DSTAMPA(9);
 
   // L4 gates (netif_event.c:1084-1127) -> which region to sum.
   uint32_t l4_gate = PENDING;
@@ -704,6 +1048,7 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
       }
     }
   }
+  DSTAMPA(10);
 
   // Sums over the staged window: IPv4 header [S3,E3); the L4 region's
   // window part: [S4,E4) when it ends inside the window, else [S4,off0)
@@ -729,6 +1074,7 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
     }
     if (cut < S4) s4 = 0u - s4;
   }
+  DSTAMPA(11);
   if (reason == PENDING && need_ip) {
     // IHL != 0 makes the word sum non-zero: fold == 0xffff <=> valid.
     if (ihl4 == 0 || fold16(s3) != 0xffffu) reason = OO_RX_R_IP4_CSUM;
@@ -810,6 +1156,7 @@ __device__ __forceinline__ Hdr parse_general(const Win& W, int shift, int len, i
       h.late = late;
     }
   }
+  DSTAMPA(12);
   return h;
 }
 
@@ -960,27 +1307,12 @@ __device__ __forceinline__ bool parse_fixed6(const uint4 (&c)[HC], int shift, in
   return true;
 }
 
-// The staged window of this lane's packet in registers (one LDS wait).
-__device__ __forceinline__ void read_cells(const Win& W, uint4 (&c)[HC]) {
-  static_assert(HC == 8, "eight window cells");
-  uint32_t a[HC];
-#pragma unroll
-  for (int k = 0; k < HC; ++k) a[k] = (uint32_t)(uintptr_t)(lptr)(W.cell(k));
-  asm volatile(
-      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\t"
-      "ds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\t"
-      "ds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\t"
-      "ds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3]), "=&v"(c[4]), "=&v"(c[5]),
-        "=&v"(c[6]), "=&v"(c[7])
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
-      : "memory");
-}
-
 // The header stage of one packet (one lane): the fixed-format paths when
 // they apply, the general walk otherwise (handle_rx_csum_bad's gates and
 // checksums, handle_rx_pkt's IPv4 checks).
+// RUNS: the general walk by word runs (win_kernel; rx_kernel, at its
+// register limit with the body ring's cursors live, keeps the byte walk).
+template <bool RUNS>
 __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, uint64_t abase) {
   const int off0 = (int)body_off0(abase);
   Hdr h;
@@ -989,15 +1321,18 @@ __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, u
     uint4 c[HC];
     read_cells(W, c);
     fixed = parse_fixed(c, shift, len, off0, h);
+    DSTAMP(13);
     if (__ballot(!fixed && (c[0].w & 0xffffu) == 0xdd86u) != 0) {
       bool f6 = false;
       if (!fixed) f6 = parse_fixed6(c, shift, len, off0, h);
       fixed = fixed || f6;
     }
   }
+  DSTAMP(14);
   if (__ballot(!fixed) != 0) {
-    if (!fixed) h = parse_general(W, shift, len, off0);
+    if (!fixed) h = RUNS ? parse_general_runs(W, shift, len, off0) : parse_general(W, shift, len, off0);
   }
+  DSTAMP(15);
   return h;
 }
 
@@ -2654,13 +2989,13 @@ __device__ __forceinline__ void tile_loop(const KParams& P) {
       th = tx_header(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
       issue_extra();
     } else {
-      const Hdr h = parse_headers(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
-      STAMP(2, __builtin_amdgcn_s_memrealtime());
 #ifdef OO_RX_STAMPS
       if (lane == 0)
         dstamp_slot(P.stamps != nullptr && it_ < 128 ? &P.stamps[((size_t)gwave * 128 + it_) * 16] : nullptr,
                     true);
 #endif
+      const Hdr h = parse_headers<false>(window_of(L.hdr, lane), dv.shift, dv.len, dv.abase);
+      STAMP(2, __builtin_amdgcn_s_memrealtime());
       ps = demux_packet(P, h, dv.intf_i, dv.abase, dv.span, dv.shift);
       issue_extra();
     }
@@ -2970,8 +3305,15 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     // This tile's windows, and the next tile's descriptors (issued before
     // them): newer are, after the first tile, the claim and the previous
     // tile's record stores.
+    STAMP(0, __builtin_amdgcn_s_memrealtime());
     if (it_ == 0) vm_wait<0>();
     else vm_wait<1 + NST>();
+    STAMP(1, __builtin_amdgcn_s_memrealtime());
+#ifdef OO_RX_STAMPS
+    if (lane == 0)
+      dstamp_slot(P.stamps != nullptr && it_ < 128 ? &P.stamps[((size_t)gwave * 128 + it_) * 16] : nullptr,
+                  true);
+#endif
     // The claim made at the last tile's staging: the tile after the next
     // one.  (Read here, not in the staging below, where the compiler's wait
     // for it would also wait for the key index loads.  Claiming at the
@@ -2986,7 +3328,8 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     // loop-long registers would spill)
     uint32_t wl = lane;
     asm volatile("" : "+v"(wl));
-    const Hdr h = parse_headers(window_of(L.hdr, wl), dv.shift, dv.len, dv.abase);
+    const Hdr h = parse_headers<OO_RX_GEN_RUNS>(window_of(L.hdr, wl), dv.shift, dv.len, dv.abase);
+    STAMP(2, __builtin_amdgcn_s_memrealtime());
     // ---- lookups and the record.  The next tile is staged inside the
     // demux, as soon as the key index's loads are issued and before they
     // are waited for, so the lookup's round trip and the staging's overlap
@@ -3009,6 +3352,8 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     };
     Parsed ps = demux_packet<true, true>(P, h, dv.intf_i, dv.abase, dv.span, dv.shift, lds_occ, stage);
 
+    STAMP(3, __builtin_amdgcn_s_memrealtime());
+    STAMP(4, __builtin_amdgcn_s_memrealtime());
     const uint32_t reason = ps.r.reason;
     store_records(P, tile, ps.r, lane);
     // The pending words of a tile holding frames with a body.
@@ -3024,6 +3369,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
       waits = waits || __ballot(wait) != 0;
     }
     if (P.counters != nullptr) cnt += reason_hist(reason, dv.valid, lane);
+    STAMP(5, __builtin_amdgcn_s_memrealtime());
     tcur = tnext;
     tnext = tnext2;
   }

@@ -133,6 +133,27 @@ def main() -> None:
             res["walk_stage_us_mean"] = [float(((q[:, 11] - q[:, 9]) * ns).mean() / 1e3),
                                          float(((q[:, 12] - q[:, 11]) * ns).mean() / 1e3),
                                          float(((q[:, 10] - q[:, 12]) * ns).mean() / 1e3)]
+    # Inside the parse (slots 13-15, when the build stamps them): the cells
+    # read and the IPv4 fixed-format parse, the IPv6 one, the general walk.
+    pm = (ph[:, 13] != 0) & (ph[:, 14] != 0) & (ph[:, 15] != 0)
+    if pm.any():
+        q = ph[pm]
+        res["parse_us_mean"] = {
+            "cells_fixed4": float(((q[:, 13] - q[:, 1]) * ns).mean() / 1e3),
+            "fixed6": float(((q[:, 14] - q[:, 13]) * ns).mean() / 1e3),
+            "general": float(((q[:, 15] - q[:, 14]) * ns).mean() / 1e3),
+            "to_stamp2": float(((q[:, 2] - q[:, 15]) * ns).mean() / 1e3),
+            "tiles": int(pm.sum())}
+        gm = pm & (ph[:, 9] != 0) & (ph[:, 12] != 0) & (ph[:, 10] != 0) & (ph[:, 11] != 0)
+        if gm.any():
+            q = ph[gm]
+            res["general_us_mean"] = {
+                "l2_l3": float(((q[:, 9] - q[:, 14]) * ns).mean() / 1e3),
+                "l4_pseudo": float(((q[:, 10] - q[:, 9]) * ns).mean() / 1e3),
+                "sums": float(((q[:, 11] - q[:, 10]) * ns).mean() / 1e3),
+                "verdict_fields_options": float(((q[:, 12] - q[:, 11]) * ns).mean() / 1e3),
+                "to_end": float(((q[:, 15] - q[:, 12]) * ns).mean() / 1e3),
+                "tiles": int(gm.sum())}
     # Phase concurrency over time: the fraction of live waves streaming a
     # body (stamps 3 -> 4) vs in the header phases (0 -> 3), in 1-us bins --
     # synchronised header phases show as dips in the streaming fraction.
