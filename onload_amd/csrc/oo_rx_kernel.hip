@@ -629,6 +629,125 @@ __device__ __forceinline__ void read_cells(const Win& W, uint4 (&c)[HC]) {
       : "memory");
 }
 
+// The eight cells and two more (by address) in one batch with one wait.
+__device__ __forceinline__ void read_cells_and(const Win& W, uint32_t ah, uint32_t at, uint4 (&c)[HC],
+                                               uint4& ch, uint4& ct) {
+  uint32_t a[HC];
+#pragma unroll
+  for (int k = 0; k < HC; ++k) a[k] = (uint32_t)(uintptr_t)(lptr)(W.cell(k));
+  asm volatile(
+      "ds_read_b128 %0, %10\n\tds_read_b128 %1, %11\n\t"
+      "ds_read_b128 %2, %12\n\tds_read_b128 %3, %13\n\t"
+      "ds_read_b128 %4, %14\n\tds_read_b128 %5, %15\n\t"
+      "ds_read_b128 %6, %16\n\tds_read_b128 %7, %17\n\t"
+      "ds_read_b128 %8, %18\n\tds_read_b128 %9, %19\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3]), "=&v"(c[4]), "=&v"(c[5]),
+        "=&v"(c[6]), "=&v"(c[7]), "=&v"(ch), "=&v"(ct)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+        "v"(ah), "v"(at)
+      : "memory");
+}
+
+// Word sum of the cell's words whose bits are set in wm (8 bits).
+__device__ __forceinline__ uint32_t cell_sum_masked(const uint4& v, uint32_t wm, uint32_t acc) {
+  auto wt = [&](int i) { return ((wm >> (2 * i)) & 1u) | (((wm >> (2 * i + 1)) & 1u) << 16); };
+  acc = dot(v.x, wt(0), acc);
+  acc = dot(v.y, wt(1), acc);
+  acc = dot(v.z, wt(2), acc);
+  return dot(v.w, wt(3), acc);
+}
+
+// Byte b (0..15) of a cell.
+__device__ __forceinline__ uint32_t cell_byte(const uint4& v, uint32_t b) {
+  const uint32_t i = b >> 2;
+  const uint32_t w = i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+  return (w >> (8 * (b & 3u))) & 0xffu;
+}
+
+// The partial-cell part of a window-word sum of window bytes [lo, hi)
+// (0 <= lo <= hi <= HB) -- words pair at even window positions: the words
+// [wlo, whi) of the head cell kh and the tail cell kt (their bytes in ch, ct),
+// an odd end's half word taken off; the cells strictly between are the
+// caller's (whole).
+struct WinSpan {
+  uint32_t wlo, whi, kh, kt;
+  bool any;
+};
+__device__ __forceinline__ WinSpan win_span(int lo, int hi) {
+  WinSpan w;
+  w.wlo = (uint32_t)lo >> 1;
+  w.whi = (uint32_t)(hi + 1) >> 1;
+  w.any = w.wlo < w.whi;
+  w.kh = w.wlo >> 3;
+  w.kt = w.any ? (w.whi - 1u) >> 3 : w.kh;
+  return w;
+}
+__device__ __forceinline__ uint32_t win_span_ends(const WinSpan& w, int lo, int hi, const uint4& ch,
+                                                  const uint4& ct, uint32_t s) {
+  const uint32_t a = w.wlo & 7u;
+  const uint32_t bh = w.kh == w.kt ? w.whi - 8u * w.kh : 8u;
+  s = cell_sum_masked(ch, w.any ? ((1u << bh) - 1u) & ~((1u << a) - 1u) : 0u, s);
+  s = cell_sum_masked(ct, w.any && w.kt != w.kh ? (1u << (w.whi - 8u * w.kt)) - 1u : 0u, s);
+  if (lo & 1) s -= cell_byte(ch, (uint32_t)(lo - 1) & 15u);
+  if (hi & 1) s -= cell_byte(ct, (uint32_t)hi & 15u) << 8;
+  return s;
+}
+
+// The whole window-word sum of [lo, hi): what chunk_sum gives summed over
+// the eight cells (read here with the two end cells, one batch).
+__device__ __forceinline__ uint32_t window_sum(const Win& W, int lo, int hi) {
+  const WinSpan w = win_span(lo, hi);
+  uint4 c[HC], ch, ct;
+  read_cells_and(W, (uint32_t)(uintptr_t)(lptr)(W.cell((int)(w.kh & 7u))),
+                 (uint32_t)(uintptr_t)(lptr)(W.cell((int)(w.kt & 7u))), c, ch, ct);
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < HC; ++k) {
+    const uint32_t t = chunk_sum_all(c[k], 0u);
+    s += ((uint32_t)k > w.kh && (uint32_t)k < w.kt) ? t : 0u;
+  }
+  return win_span_ends(w, lo, hi, ch, ct, s);
+}
+
+// The same from cells already in registers (the end cells read again from
+// LDS: a register array indexed per lane would go through scratch); only
+// cells from KMIN on can lie inside.
+template <int KMIN>
+__device__ __forceinline__ uint32_t window_sum_cells(const Win& W, const uint4 (&c)[HC], int lo, int hi) {
+  const WinSpan w = win_span(lo, hi);
+  uint4 ch, ct;
+  {
+    const uint32_t ah = (uint32_t)(uintptr_t)(lptr)(W.cell((int)(w.kh & 7u)));
+    const uint32_t at = (uint32_t)(uintptr_t)(lptr)(W.cell((int)(w.kt & 7u)));
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(ch), "=&v"(ct)
+                 : "v"(ah), "v"(at)
+                 : "memory");
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = KMIN; k < HC; ++k) {
+    const bool in = (uint32_t)k > w.kh && (uint32_t)k < w.kt;
+    if (__ballot(in) != 0) s += in ? chunk_sum_all(c[k], 0u) : 0u;  // (short regions: no lane)
+  }
+  return win_span_ends(w, lo, hi, ch, ct, s);
+}
+
+// Window bytes q and q + 1 (q + 1 < HB), low half: two byte reads, one wait.
+__device__ __forceinline__ uint32_t win_byte_pair(const Win& W, uint32_t q) {
+  const uint32_t row = (uint32_t)(uintptr_t)(lptr)(W.row);
+  const uint32_t r = q + 1u;
+  const uint32_t a0 = row + ((((q >> 4) + W.rot) & 7u) << 4) + (q & 15u);
+  const uint32_t a1 = row + ((((r >> 4) + W.rot) & 7u) << 4) + (r & 15u);
+  uint32_t b0, b1;
+  asm volatile("ds_read_u8 %0, %2\n\tds_read_u8 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(b0), "=&v"(b1)
+               : "v"(a0), "v"(a1)
+               : "memory");
+  return b0 | (b1 << 8);
+}
+
 // K aligned 4-byte LDS reads in one batch with one wait.
 template <int K>
 __device__ __forceinline__ void lds_read_b32s(const uint32_t (&a)[K], uint32_t (&d)[K]);
@@ -680,19 +799,6 @@ __device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t if0, uint32_t if1)
   uint32_t r;
   asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
   return r;
-}
-
-// Bytes r, r + 1 of the option words O (r < 40) in the low half.
-__device__ __forceinline__ uint32_t opt_pair(const uint32_t (&O)[10], int r) {
-  const uint32_t i = (uint32_t)r >> 2;
-  uint32_t lo = O[0], hi = O[1];
-#pragma unroll
-  for (int k = 1; k < 10; ++k) {
-    const uint64_t m = __ballot(i == (uint32_t)k);
-    lo = vsel(m, lo, O[k]);
-    hi = vsel(m, hi, k + 1 < 10 ? O[k + 1] : 0u);
-  }
-  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)r & 3u);
 }
 
 // Bit i: option byte i is not IPOPT_NOP (bytes 0..39).
@@ -851,11 +957,7 @@ __device__ __forceinline__ Hdr parse_general_runs(const Win& W, int shift, int l
     for (int k = 0; k < 10; ++k) s3 = dot(O[k], k < nopt ? 0x00010001u : 0u, s3);
   }
   if (need_l4) {
-    uint4 c[HC];  // (read again: held across the walk they cost a spill)
-    read_cells(W, c);
-#pragma unroll
-    for (int k = 0; k < HC; ++k)
-      if (k * 16 < hi4) s4 += chunk_sum(c[k], k * 16, lo4, hi4);
+    s4 = window_sum(W, lo4, hi4);
     if (cut < S4) s4 = 0u - s4;
   }
   if (reason == PENDING && need_ip) {
@@ -920,7 +1022,7 @@ __device__ __forceinline__ Hdr parse_general_runs(const Win& W, int shift, int l
           const uint64_t rest = nn >> o;
           o += rest != 0 ? (int)__builtin_ctzll(rest) : 64;
           if (o >= end) break;
-          const uint32_t b2 = opt_pair(O, o);
+          const uint32_t b2 = win_byte_pair(W, (uint32_t)(shift + l3 + 20 + o));
           const uint32_t kind = b2 & 0xffu;
           if (kind == 0u) break;  // IPOPT_EOL
           if (kind == 7u || kind == 68u || kind == 130u || kind == 136u) {
@@ -1168,8 +1270,15 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xffu) <<
 // of the eight staged cells c[] (window bytes 16k..16k+15 in c[k]) with
 // shifts; the same decisions as parse_general for these frames.  Returns
 // false (h untouched beyond scratch) for every other frame.
-__device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int len, int off0,
-                                            Hdr& h) {
+#ifndef OO_RX_FIXED_SPAN
+#define OO_RX_FIXED_SPAN 1
+#endif
+// SPAN: a region ending inside a cell is summed as one span (the cells
+// between whole, the end cells masked: window_sum_cells) instead of cell by
+// cell (win_kernel; rx_kernel is at its register limit).
+template <bool SPAN>
+__device__ __forceinline__ bool parse_fixed(const Win& W, const uint4 (&c)[HC], int shift, int len,
+                                            int off0, Hdr& h) {
   const uint32_t ip_len = bswap16(c[1].x);
   const uint32_t frag = bswap16(c[1].y);
   const uint32_t proto = c[1].y >> 24;
@@ -1204,6 +1313,8 @@ __device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int
       s4 += E4h >= 16 * k + 16 ? t : 0u;
     }
     s4 -= E4h >= 48 ? (c[2].x & 0xffffu) : 0u;  // bytes 32-33: the IPv4 header's
+  } else if (SPAN) {
+    s4 = window_sum_cells<2>(W, c, 34, E4h);
   } else {
 #pragma unroll
     for (int k = 2; k < HC; ++k)
@@ -1241,8 +1352,9 @@ __device__ __forceinline__ bool parse_fixed(const uint4 (&c)[HC], int shift, int
 // header walk) whose length fields pass the gates.  L3 at window byte 14,
 // addresses at 22 and 38, L4 at 54.  The same decisions as parse_general for
 // these frames; false (h untouched) for every other frame.
-__device__ __forceinline__ bool parse_fixed6(const uint4 (&c)[HC], int shift, int len, int off0,
-                                             Hdr& h) {
+template <bool SPAN>
+__device__ __forceinline__ bool parse_fixed6(const Win& W, const uint4 (&c)[HC], int shift, int len,
+                                             int off0, Hdr& h) {
   const int ip_paylen = (int)bswap16(c[1].x >> 16);
   const uint32_t proto = c[1].y & 0xffu;
   const uint32_t udp_len = bswap16(c[3].z >> 16);
@@ -1271,6 +1383,8 @@ __device__ __forceinline__ bool parse_fixed6(const uint4 (&c)[HC], int shift, in
       s4 += E4h >= 16 * k + 16 ? t : 0u;
     }
     s4 -= E4h >= 64 ? (c[3].x & 0xffffu) + (c[3].x >> 16) + (c[3].y & 0xffffu) : 0u;  // [48, 54)
+  } else if (SPAN) {
+    s4 = window_sum_cells<3>(W, c, 54, E4h);
   } else {
 #pragma unroll
     for (int k = 3; k < HC; ++k)
@@ -1320,11 +1434,11 @@ __device__ __forceinline__ Hdr parse_headers(const Win& W, int shift, int len, u
   {
     uint4 c[HC];
     read_cells(W, c);
-    fixed = parse_fixed(c, shift, len, off0, h);
+    fixed = parse_fixed<RUNS && OO_RX_FIXED_SPAN>(W, c, shift, len, off0, h);
     DSTAMP(13);
     if (__ballot(!fixed && (c[0].w & 0xffffu) == 0xdd86u) != 0) {
       bool f6 = false;
-      if (!fixed) f6 = parse_fixed6(c, shift, len, off0, h);
+      if (!fixed) f6 = parse_fixed6<RUNS && OO_RX_FIXED_SPAN>(W, c, shift, len, off0, h);
       fixed = fixed || f6;
     }
   }
