@@ -195,7 +195,7 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4& v, int p, int S, int 
   return s;
 }
 
-#if (defined(OO_RX_STAMPS) || defined(OO_RX_BOUND_NOLOOK) || defined(OO_RX_BOUND_NOBODY) || \
+#if (defined(OO_RX_STAMPS) || defined(OO_RX_PAD_VALU) || defined(OO_RX_BOUND_NOLOOK) || defined(OO_RX_BOUND_NOBODY) || \
      defined(OO_RX_BOUND_KXLINE) || defined(OO_RX_BOUND_KX1) || defined(OO_RX_BOUND_NOGENSUM)) && \
     !defined(OO_RX_EXPERIMENTS)
 #error "OO_RX_STAMPS is a diagnostic build (tools/build_ref.sh sets OO_RX_EXPERIMENTS)"
@@ -3468,6 +3468,24 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
 
     STAMP(3, __builtin_amdgcn_s_memrealtime());
     STAMP(4, __builtin_amdgcn_s_memrealtime());
+#ifdef OO_RX_PAD_VALU  // (experiment: N dependent VALU instructions per tile, nothing else)
+    {
+#ifdef OO_RX_PADI  // eight independent chains: the issue cost without the latency
+      uint32_t pad[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pad[j] = lane + j;
+#pragma unroll
+      for (int i = 0; i < OO_RX_PAD_VALU; ++i) asm volatile("v_add_u32 %0, 1, %0" : "+v"(pad[i & 7]));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(pad[j]));
+#else
+      uint32_t pad = lane;
+#pragma unroll
+      for (int i = 0; i < OO_RX_PAD_VALU; ++i) asm volatile("v_add_u32 %0, 1, %0" : "+v"(pad));
+      asm volatile("" ::"v"(pad));
+#endif
+    }
+#endif
     const uint32_t reason = ps.r.reason;
     store_records(P, tile, ps.r, lane);
     // The pending words of a tile holding frames with a body.
