@@ -1884,6 +1884,24 @@ int oo_gpu_rx_debug_stamps(oo_gpu_rx_ctx* c, void* d_buf) {
 
 int oo_gpu_rx_debug_grid(oo_gpu_rx_ctx* c) { return c ? (int)c->grid : -EINVAL; }
 
+#ifdef OO_RX_EXPERIMENTS
+// Diagnostic (experiment builds): the key index's arrays copied to host
+// memory after pending table changes are applied, and its sizes.
+extern "C" int oo_gpu_rx_debug_kx(oo_gpu_rx_ctx* c, void* h4, uint64_t b4, void* h6, uint64_t b6,
+                                  uint32_t* nb4_ne6) {
+  if (c == nullptr || c->T.kx4 == nullptr) return -EINVAL;
+  if (prepare(c, c->stream) != 0) return -EIO;
+  nb4_ne6[0] = c->T.kx_nb4;
+  nb4_ne6[1] = c->T.kx_ne6;
+  if (hipDeviceSynchronize() != hipSuccess) return -EIO;
+  if (b4 > oo_table_kx_bytes4(c->T.kx_nb4) || b6 > oo_table_kx_bytes6(c->T.kx_ne6)) return -EINVAL;
+  if (hipMemcpy(h4, c->T.kx4, b4, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(h6, c->T.kx6, b6, hipMemcpyDeviceToHost) != hipSuccess)
+    return -EIO;
+  return 0;
+}
+#endif
+
 const char* oo_gpu_rx_reason_str(int r) {
   switch (r) {
     case OO_RX_R_DELIVER: return "DELIVER";

@@ -161,12 +161,19 @@ OO_HD uint32_t kx_mix(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
-// The key hash: IPv4 keys with la[1..3] = ra[1..3] = 0 and pw = 0.
+// The key hash: IPv4 keys with la[1..3] = ra[1..3] = 0 and pw = 0.  Each
+// word's high half is folded into its low half before the multiply: the
+// words hold network-order bytes, so a key's varying octets (the peer's last
+// address byte, the ports) sit in the high bits, which a multiply never
+// carries down -- without the fold, config 5's 4,160 TCP keys shared a home
+// bucket 12x as often as random keys would (tools/kx_probe.py).
+OO_HD uint32_t kx_fold(uint32_t w) { return w ^ (w >> 16); }
 OO_HD uint32_t kx_hash(uint32_t la0, uint32_t la1, uint32_t la2, uint32_t la3, uint32_t ra0,
                        uint32_t ra1, uint32_t ra2, uint32_t ra3, uint32_t ports, uint32_t pw) {
-  return kx_mix(la0 * 0x9e3779b1u + la1 * 0x85ebca77u + la2 * 0xc2b2ae3du + la3 * 0x27d4eb2fu +
-                ra0 * 0x165667b1u + ra1 * 0xd3a2646du + ra2 * 0xfd7046c5u + ra3 * 0xb55a4f09u +
-                ports * 0x2545f491u + pw * 0x9e3779b9u);
+  return kx_mix(kx_fold(la0) * 0x9e3779b1u + kx_fold(la1) * 0x85ebca77u + kx_fold(la2) * 0xc2b2ae3du +
+                kx_fold(la3) * 0x27d4eb2fu + kx_fold(ra0) * 0x165667b1u + kx_fold(ra1) * 0xd3a2646du +
+                kx_fold(ra2) * 0xfd7046c5u + kx_fold(ra3) * 0xb55a4f09u + kx_fold(ports) * 0x2545f491u +
+                kx_fold(pw) * 0x9e3779b9u);
 }
 
 // Device-resident filter-table state of a context.

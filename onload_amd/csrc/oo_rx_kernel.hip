@@ -1863,7 +1863,9 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
   // The first level is issued at once (a loop head would first wait for
   // every load in flight, the body stream's included); the loop takes the
   // rare keys whose bucket was full.
+  DSTAMP(9);
   level(true);
+  DSTAMP(10);
   bool left = false;
   for (uint32_t it = 1;; ++it) {
     const bool any = pend[0] || pend[1] || pend[2];
@@ -1874,6 +1876,7 @@ __device__ __forceinline__ bool kx_lookup(const KParams& P, const Hdr& h, bool l
     }
     level(false);
   }
+  DSTAMP(11);
   asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(okw));
   const bool f0 = val[0] != 0u, f1 = val[1] != 0u, f2 = tcp && val[2] != 0u;
   bool fb = left;
@@ -2036,6 +2039,7 @@ __device__ __forceinline__ Parsed demux_packet_t(const KParams& P, const Hdr& h,
   } else {
     issued();
   }
+  DSTAMP(12);
   oo_gpu_rx_result r;
   r.reason = 0; r.flags = 0; r.stage = 0; r.proto = 0; r.vlan = (uint16_t)vlan;
   r.l4_off = 0; r.ip_paylen = 0; r.sport_be = 0; r.dport_be = 0; r.nmatch = 0;

@@ -46,11 +46,13 @@ _C = [0x9E3779B1, 0x85EBCA77, 0xC2B2AE3D, 0x27D4EB2F, 0x165667B1, 0xD3A2646D, 0x
 
 
 def kx_hash(words):
-    """oo_rx_device.h kx_hash over ten uint32 arrays (la[4], ra[4], ports, pw)."""
+    """oo_rx_device.h kx_hash over ten uint32 arrays (la[4], ra[4], ports, pw):
+    each word folded (w ^ w >> 16), weighted, summed, mixed."""
     with np.errstate(over="ignore"):
         acc = np.zeros(np.broadcast(*words).shape, dtype=np.uint32)
         for w, c in zip(words, _C):
-            acc = acc + np.asarray(w, dtype=np.uint32) * np.uint32(c)
+            w = np.asarray(w, dtype=np.uint32)
+            acc = acc + (w ^ (w >> np.uint32(16))) * np.uint32(c)
         return _mix(acc)
 
 

@@ -133,6 +133,18 @@ def main() -> None:
             res["walk_stage_us_mean"] = [float(((q[:, 11] - q[:, 9]) * ns).mean() / 1e3),
                                          float(((q[:, 12] - q[:, 11]) * ns).mean() / 1e3),
                                          float(((q[:, 10] - q[:, 12]) * ns).mean() / 1e3)]
+    # The demux as a chain of its stamps (2 -> 8 -> 9 -> 10 -> 11 -> 12 -> 3),
+    # over the tiles that have them all (builds that stamp the key index's
+    # levels: 9 before, 10 after the first, 11 after the last; 12 before the
+    # record's assembly).
+    res["slot_nonzero_frac"] = [round(float((ph[:, j] != 0).mean()), 3) for j in range(16)]
+    chain = [2, 8, 9, 10, 11, 12, 3]
+    cm = np.all(ph[:, chain] != 0, axis=1) & ~((ph[:, 11] >= 1000000) & (ph[:, 11] < 2000000))
+    if cm.any():
+        q = ph[cm]
+        res["demux_chain_us"] = {f"{i}->{j}": float(((q[:, j] - q[:, i]) * ns).mean() / 1e3)
+                                 for i, j in zip(chain, chain[1:])}
+        res["demux_chain_tiles"] = int(cm.sum())
     # Inside the parse (slots 13-15, when the build stamps them): the cells
     # read and the IPv4 fixed-format parse, the IPv6 one, the general walk.
     pm = (ph[:, 13] != 0) & (ph[:, 14] != 0) & (ph[:, 15] != 0)
