@@ -137,6 +137,10 @@ def main() -> None:
     # over the tiles that have them all (builds that stamp the key index's
     # levels: 9 before, 10 after the first, 11 after the last; 12 before the
     # record's assembly).
+    # (builds that stamp the index's level count as 4000000 + levels in slot 11)
+    lvm = (ph[:, 11] >= 4000000) & (ph[:, 11] < 5000000)
+    if lvm.any():
+        res["kx_levels_hist"] = np.bincount((ph[lvm, 11] - 4000000).astype(np.int64)).tolist()
     res["slot_nonzero_frac"] = [round(float((ph[:, j] != 0).mean()), 3) for j in range(16)]
     chain = [2, 8, 9, 10, 11, 12, 3]
     cm = np.all(ph[:, chain] != 0, axis=1) & ~((ph[:, 11] >= 1000000) & (ph[:, 11] < 2000000))
