@@ -2950,6 +2950,11 @@ __device__ __forceinline__ void vm_wait_n(int n) {
 // issues exactly NST stores and needs no per-lane sink address (tiles are
 // never empty: the host's partition, oo_gpu_rx.cpp launch()).  All lanes
 // active.
+// DIRECT: each lane stores its own record (two 16-B stores at a 32-B
+// stride; win_kernel: config 3 -2.5 %) instead of the lane-permuted 1-KiB
+// runs (rx_kernel, where the direct form measured +1.2 % on config 2:
+// profiles/r06/ab_rec_direct_c2-5.log).
+template <bool DIRECT = false>
 __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
                                               const oo_gpu_rx_result& r, uint32_t lane) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
@@ -2960,6 +2965,13 @@ __device__ __forceinline__ void store_records(const KParams& P, const Unit& t,
   // lgkmcnt as well)
   __attribute__((address_space(1))) u32x4* const out =
       (__attribute__((address_space(1))) u32x4*)reinterpret_cast<uintptr_t>(P.out);
+  if constexpr (DIRECT) {
+    if (lane < t.cnt) {
+      out[(size_t)(t.first + lane) * 2u] = u32x4{w[0], w[1], w[2], w[3]};
+      out[(size_t)(t.first + lane) * 2u + 1u] = u32x4{w[4], w[5], w[6], w[7]};
+    }
+    return;
+  }
 #pragma unroll
   for (uint32_t u = 0; u < 2; ++u) {
     const uint32_t q = min(32u * u + (lane >> 1), last);
@@ -3405,6 +3417,9 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
 #ifndef OO_RX_WIN_HDR_AUX
 #define OO_RX_WIN_HDR_AUX 2
 #endif
+#ifndef OO_RX_WIN_REC_DIRECT
+#define OO_RX_WIN_REC_DIRECT 1  // each lane stores its own record (store_records)
+#endif
   bool clean = false;
   // Prologue: tile t0's descriptors, then t1's and t0's windows.
   {
@@ -3491,7 +3506,7 @@ __device__ __forceinline__ void window_loop(const KParams& P) {
     }
 #endif
     const uint32_t reason = ps.r.reason;
-    store_records(P, tile, ps.r, lane);
+    store_records<OO_RX_WIN_REC_DIRECT>(P, tile, ps.r, lane);
     // The pending words of a tile holding frames with a body.
     const bool body = dv.span > HB;
     if (__ballot(body) != 0) {
