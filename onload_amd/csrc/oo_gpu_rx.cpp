@@ -122,7 +122,7 @@ static_assert(sizeof(Entry4) == 8 && sizeof(Ext4) == 8 && sizeof(Entry6) == 24,
 #define OO_KX_V4_MUL 1  // IPv4 buckets per protocol region per table slot
 #endif
 #ifndef OO_KX_V6_MUL
-#define OO_KX_V6_MUL 4  // IPv6 index entries per table slot
+#define OO_KX_V6_MUL 8  // IPv6 index entries per table slot (8: config 5 -0.3 % against 4, profiles/r06/ab_kx_sizes_c4_c5.log)
 #endif
 constexpr uint32_t OPS_CHUNK = 8192;  // table ops per device flush chunk (512 KiB)
 constexpr uint32_t SMALL_N = 2048;    // launch(): batches up to this many packets take 8-packet tiles

@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 NTHREADS = min(16, os.cpu_count() or 1)
 HWPORTS = (0, 1, 3, 2, 5)
 NB4 = 1 << 16  # buckets per protocol region for a 2^16-slot IPv4 table
-NE6 = 1 << 16  # IPv6 entries for a 2^14-slot IPv6 table
+NE6 = 1 << 17  # IPv6 entries for a 2^14-slot IPv6 table (OO_KX_V6_MUL 8)
 
 
 @pytest.fixture(scope="module")
@@ -74,7 +74,7 @@ def colliding_v4(n, lport0=20000, nports=256):
 
 def colliding_v6(n, lport=21000):
     """n IPv6 UDP wildcard keys (fd00::x:y, lport) in one IPv6 index entry run."""
-    lo = np.arange(1 << 22, dtype=np.uint32)
+    lo = np.arange(1 << 23, dtype=np.uint32)
     base = L6A[:12]
     w = [np.uint32(_le(base[4 * i:4 * i + 4])) for i in range(3)]
     la3 = lo.byteswap()  # the last word as the frame holds it (network order)
